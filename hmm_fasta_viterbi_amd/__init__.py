@@ -1,0 +1,198 @@
+"""hmm_fasta_viterbi_amd -- MI355X-native MSV (Multiple Segment Viterbi) scoring engine.
+
+Python mirror of the reference's C++ class surface, bound to libmsv_hip.so (include/msv.h):
+
+    Profile_HMM(path)                       data_readers/Profile_HMM.hpp:21-49
+    FASTA_protein_sequences(path)           data_readers/FASTA_protein_sequences.hpp:9-14
+    MSV_HMM(profile).run_on_sequence(seq)   algorithms/MSV_HMM.hpp:17-44
+                    .parallel_run_on_sequence(seq, should_specialize=False)
+                    .score_batch(...)       (new: one fused kernel launch per batch)
+
+Sequences use the reference's form ('#' sentinel + one-letter residues) or packed codes
+0..19 (alphabetical A C D E F G H I K L M N P Q R S T V W Y) with CSR offsets.
+Every score is computed by the hand-written gfx950 kernel; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import _native
+from ._native import MSVError, check
+
+__all__ = [
+    "AMINO_ACIDS", "MSVError", "Profile_HMM", "FASTA_protein_sequences", "MSV_HMM", "pack_sequences",
+    "encode", "sequence_transitions", "device_count",
+]
+
+AMINO_ACIDS = "ACDEFGHIKLMNPQRSTVWY"  # MSV_HMM.cpp:29-31
+_LUT = np.full(256, 254, np.uint8)
+for _i, _c in enumerate(AMINO_ACIDS):
+    _LUT[ord(_c)] = _i
+_LUT[ord("#")] = 255
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    _native.lib().msv_device_count(C.byref(n))
+    return n.value
+
+
+def sequence_transitions(L: int) -> tuple[float, float]:
+    """(tr_loop, tr_move) of MSV_HMM::init_transitions_depend_on_seq (MSV_HMM.cpp:59-64)."""
+    a, b = C.c_float(), C.c_float()
+    _native.lib().msv_sequence_transitions(L, C.byref(a), C.byref(b))
+    return a.value, b.value
+
+
+def encode(residues: str) -> np.ndarray:
+    """One-letter residues (no '#') -> codes 0..19; IndexError on anything else (the
+    reference's amino_acid_num.at throws std::out_of_range, MSV_HMM.cpp:101)."""
+    codes = _LUT[np.frombuffer(residues.encode("latin-1"), np.uint8)]
+    if codes.size and codes.max() >= 20:
+        raise IndexError("residue outside the 20 amino acids")
+    return codes
+
+
+def pack_sequences(seqs: Sequence[str]) -> tuple[np.ndarray, np.ndarray]:
+    """'#'-prefixed sequences -> (codes uint8, offsets uint64[n+1])."""
+    lens = np.fromiter((max(len(s) - 1, 0) for s in seqs), np.uint64, count=len(seqs))
+    offsets = np.zeros(len(seqs) + 1, np.uint64)
+    np.cumsum(lens, out=offsets[1:])
+    body = "".join(s[1:] for s in seqs)
+    return encode(body), offsets
+
+
+class Profile_HMM:
+    """Parsed HMMER3 profile (C++ parser in libmsv_hip.so, Profile_HMM.cpp:48-60 semantics)."""
+
+    def __init__(self, file_path: str):
+        L = _native.lib()
+        h = C.c_void_p()
+        check(L.msv_hmm_read(str(file_path).encode(), C.byref(h)), f"Profile_HMM({file_path})")
+        self._h = h
+        self.path = str(file_path)
+        self.model_length = int(L.msv_hmm_model_length(h))
+        self.name = L.msv_hmm_name(h).decode("latin-1")
+        st = (C.c_float * 6)()
+        L.msv_hmm_stats(h, st)
+        (self.stats_local_msv_mu, self.stats_local_msv_lambda, self.stats_local_viterbi_mu,
+         self.stats_local_viterbi_lambda, self.stats_local_forward_theta,
+         self.stats_local_forward_lambda) = [float(np.float32(x)) for x in st]
+        M = self.model_length
+        self.match_emissions = np.ctypeslib.as_array(L.msv_hmm_match_emissions(h), (M, 20)).copy()
+        self.insert_emissions = np.ctypeslib.as_array(L.msv_hmm_insert_emissions(h), (M, 20)).copy()
+        self.transitions = np.ctypeslib.as_array(L.msv_hmm_transitions(h), (M, 7)).copy()
+
+    def msv_scores(self) -> tuple[np.ndarray, float, float, float]:
+        """MSV host precompute (MSV_HMM.cpp:35-57): ([20, M] log-odds, tr_B_Mk, tr_E_C, tr_E_J)."""
+        es = np.zeros((20, self.model_length), np.float32)
+        b, c, j = C.c_float(), C.c_float(), C.c_float()
+        check(_native.lib().msv_hmm_msv_scores(self._h, es.ctypes.data_as(C.POINTER(C.c_float)), C.byref(b),
+                                                C.byref(c), C.byref(j)))
+        return es, b.value, c.value, j.value
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _native._lib is not None:
+            _native._lib.msv_hmm_destroy(self._h)
+            self._h = None
+
+
+class FASTA_protein_sequences:
+    """FASTA reader (FASTA_protein_sequences.cpp:9-44 semantics), packed straight to codes."""
+
+    def __init__(self, file_path: str):
+        L = _native.lib()
+        f = C.c_void_p()
+        check(L.msv_fasta_read(str(file_path).encode(), C.byref(f)), f"FASTA_protein_sequences({file_path})")
+        try:
+            n = int(L.msv_fasta_count(f))
+            self.offsets = np.ctypeslib.as_array(L.msv_fasta_offsets(f), (n + 1,)).copy()
+            total = int(self.offsets[-1])
+            self.codes = (np.ctypeslib.as_array(L.msv_fasta_codes(f), (total,)).copy() if total
+                          else np.zeros(0, np.uint8))
+            self.headers = [L.msv_fasta_header(f, i).decode("latin-1") for i in range(n)]
+            self.rejected = int(L.msv_fasta_rejected(f))
+        finally:
+            L.msv_fasta_destroy(f)
+        letters = np.frombuffer((AMINO_ACIDS + "#").encode(), np.uint8)
+        text = letters[np.minimum(self.codes, 20)].tobytes().decode()
+        self.sequences = ["#" + text[self.offsets[i]:self.offsets[i + 1]] for i in range(n)]
+
+    def __len__(self):
+        return len(self.sequences)
+
+
+class MSV_HMM:
+    """MSV scorer for one profile on one GPU (MSV_HMM.hpp:17-44); every score comes from the
+    fused gfx950 kernel.  Not thread-safe per instance, like the reference."""
+
+    def __init__(self, base_hmm: Profile_HMM, device: int = 0):
+        L = _native.lib()
+        self.model_length = base_hmm.model_length
+        self.emission_scores, self.tr_B_Mk, self.tr_E_C, self.tr_E_J = base_hmm.msv_scores()
+        p = C.c_void_p()
+        es = np.ascontiguousarray(self.emission_scores)
+        check(L.msv_profile_create(device, es.ctypes.data, self.model_length, self.tr_B_Mk, self.tr_E_C,
+                                   self.tr_E_J, C.byref(p)), "msv_profile_create")
+        self._p = p
+        self.device = device
+
+    # -- reference surface ------------------------------------------------------------------
+    def run_on_sequence(self, seq: str) -> float:
+        return float(self.score_batch([seq])[0])
+
+    def parallel_run_on_sequence(self, seq: str, should_specialize: bool = False) -> float:
+        # should_specialize (JIT -D constants, MSV_HMM.cpp:322-337) is always on here: the kernel
+        # is a compile-time specialisation on (G, S); both settings return the same score.
+        return self.run_on_sequence(seq)
+
+    # -- batch API --------------------------------------------------------------------------
+    def score_batch(self, seqs: Sequence[str] | None = None, *, codes: np.ndarray | None = None,
+                    offsets: np.ndarray | None = None) -> np.ndarray:
+        if seqs is not None:
+            codes, offsets = pack_sequences(seqs)
+        codes = np.ascontiguousarray(codes, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        n = len(offsets) - 1
+        out = np.zeros(n, np.float32)
+        st = _native.lib().msv_score_batch(self._p, codes.ctypes.data if codes.size else None, offsets.ctypes.data,
+                                           n, out.ctypes.data, None)
+        if st == _native.MSV_ERR_BAD_RESIDUE:
+            raise IndexError("residue outside the 20 amino acids")
+        check(st, "msv_score_batch")
+        return out
+
+    def score_batch_device(self, residues_ptr: int, residues_len: int, offsets_ptr: int, n: int, scores_ptr: int,
+                           order_ptr: int | None = None, stream: int | None = None) -> None:
+        """Device-resident batch (raw device pointers, e.g. torch tensor .data_ptr()); async on
+        `stream` (a hipStream_t handle, e.g. torch.cuda.current_stream().cuda_stream)."""
+        check(_native.lib().msv_score_batch_device(self._p, residues_ptr, residues_len, offsets_ptr, n, order_ptr,
+                                                   scores_ptr, stream), "msv_score_batch_device")
+
+    def order_longest_first(self, offsets_ptr: int, n: int, order_ptr: int, stream: int | None = None) -> None:
+        check(_native.lib().msv_order_longest_first(self._p, offsets_ptr, n, order_ptr, stream))
+
+    def check(self, stream: int | None = None) -> None:
+        st = _native.lib().msv_profile_check(self._p, stream)
+        if st == _native.MSV_ERR_BAD_RESIDUE:
+            raise IndexError("residue outside the 20 amino acids")
+        check(st, "msv_profile_check")
+
+    def reserve_length(self, max_length: int) -> None:
+        check(_native.lib().msv_profile_reserve_length(self._p, max_length))
+
+    def describe(self) -> dict:
+        info = _native.KernelInfo()
+        check(_native.lib().msv_profile_describe(self._p, C.byref(info)))
+        return info.as_dict()
+
+    def close(self):
+        if getattr(self, "_p", None) and _native._lib is not None:
+            _native._lib.msv_profile_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.close()

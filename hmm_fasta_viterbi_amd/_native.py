@@ -1,0 +1,126 @@
+"""ctypes binding of the C-ABI in include/msv.h (libmsv_hip.so, built in-tree).
+
+There is no fallback: if the shared library is missing the import of the device path fails
+loudly with a message saying how to build it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libmsv_hip.so")
+
+STATUS = {
+    0: "MSV_OK",
+    1: "MSV_ERR_INVALID_ARGUMENT",
+    2: "MSV_ERR_IO",
+    3: "MSV_ERR_PARSE",
+    4: "MSV_ERR_BAD_RESIDUE",
+    5: "MSV_ERR_SEQUENCE_TOO_LONG",
+    6: "MSV_ERR_UNSUPPORTED_MODEL",
+    7: "MSV_ERR_NO_DEVICE",
+    8: "MSV_ERR_HIP",
+    9: "MSV_ERR_OUT_OF_MEMORY",
+}
+MSV_OK = 0
+MSV_ERR_BAD_RESIDUE = 4
+
+# Every symbol include/msv.h declares (checked by tests/test_capi.py).
+EXPORTED = [
+    "msv_status_string", "msv_version", "msv_device_count",
+    "msv_hmm_read", "msv_hmm_destroy", "msv_hmm_model_length", "msv_hmm_name", "msv_hmm_stats",
+    "msv_hmm_match_emissions", "msv_hmm_insert_emissions", "msv_hmm_transitions", "msv_hmm_msv_scores",
+    "msv_sequence_transitions",
+    "msv_fasta_read", "msv_fasta_destroy", "msv_fasta_count", "msv_fasta_rejected", "msv_fasta_codes",
+    "msv_fasta_offsets", "msv_fasta_header", "msv_encode_residues",
+    "msv_profile_create", "msv_profile_create_from_hmm", "msv_profile_destroy", "msv_profile_describe",
+    "msv_profile_reserve_length", "msv_score_batch", "msv_score_batch_device", "msv_profile_check",
+    "msv_order_longest_first",
+]
+
+
+class MSVError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        self.name = STATUS.get(status, f"MSV_ERR_{status}")
+        super().__init__(f"{what}: {self.name}" if what else self.name)
+
+
+class KernelInfo(C.Structure):
+    _fields_ = [
+        ("model_length", C.c_uint32),
+        ("lanes_per_group", C.c_uint32),
+        ("states_per_lane", C.c_uint32),
+        ("waves_per_block", C.c_uint32),
+        ("lds_rows", C.c_uint32),
+        ("lds_bytes", C.c_uint32),
+        ("blocks", C.c_uint32),
+        ("max_length", C.c_uint32),
+        ("device", C.c_int),
+        ("variant", C.c_char * 64),
+    ]
+
+    def as_dict(self) -> dict:
+        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d["variant"] = self.variant.decode()
+        return d
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: the MSV HIP library is not built. "
+            "Run `python -c 'import __graft_entry__ as g; g.build()'` or `make -C hmm_fasta_viterbi_amd/csrc`.")
+    L = C.CDLL(LIB_PATH)
+    vp, sz, u64, u32, f32 = C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint32, C.c_float
+    fp = C.POINTER(C.c_float)
+    sig = {
+        "msv_status_string": (C.c_char_p, [C.c_int]),
+        "msv_version": (C.c_char_p, []),
+        "msv_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+        "msv_hmm_read": (C.c_int, [C.c_char_p, C.POINTER(vp)]),
+        "msv_hmm_destroy": (None, [vp]),
+        "msv_hmm_model_length": (sz, [vp]),
+        "msv_hmm_name": (C.c_char_p, [vp]),
+        "msv_hmm_stats": (None, [vp, fp]),
+        "msv_hmm_match_emissions": (fp, [vp]),
+        "msv_hmm_insert_emissions": (fp, [vp]),
+        "msv_hmm_transitions": (fp, [vp]),
+        "msv_hmm_msv_scores": (C.c_int, [vp, fp, fp, fp, fp]),
+        "msv_sequence_transitions": (None, [u64, fp, fp]),
+        "msv_fasta_read": (C.c_int, [C.c_char_p, C.POINTER(vp)]),
+        "msv_fasta_destroy": (None, [vp]),
+        "msv_fasta_count": (sz, [vp]),
+        "msv_fasta_rejected": (sz, [vp]),
+        "msv_fasta_codes": (C.POINTER(C.c_uint8), [vp]),
+        "msv_fasta_offsets": (C.POINTER(C.c_uint64), [vp]),
+        "msv_fasta_header": (C.c_char_p, [vp, sz]),
+        "msv_encode_residues": (C.c_int, [C.c_char_p, sz, vp]),
+        "msv_profile_create": (C.c_int, [C.c_int, vp, u32, f32, f32, f32, C.POINTER(vp)]),
+        "msv_profile_create_from_hmm": (C.c_int, [C.c_int, vp, C.POINTER(vp)]),
+        "msv_profile_destroy": (None, [vp]),
+        "msv_profile_describe": (C.c_int, [vp, C.POINTER(KernelInfo)]),
+        "msv_profile_reserve_length": (C.c_int, [vp, u64]),
+        "msv_score_batch": (C.c_int, [vp, vp, vp, u64, vp, vp]),
+        "msv_score_batch_device": (C.c_int, [vp, vp, u64, vp, u64, vp, vp, vp]),
+        "msv_profile_check": (C.c_int, [vp, vp]),
+        "msv_order_longest_first": (C.c_int, [vp, vp, u64, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(status: int, what: str = "") -> None:
+    if status != MSV_OK:
+        raise MSVError(status, what)

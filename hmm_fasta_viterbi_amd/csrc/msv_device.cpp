@@ -1,0 +1,423 @@
+// msv_device.cpp -- C-ABI of the device hot path (msv.h) on the HIP runtime.
+//
+// Replaces the per-call OpenCL orchestration of MSV_HMM::parallel_run_on_sequence
+// (algorithms/MSV_HMM.cpp:269-430: a context, 23 buffers, a JIT program build and 9-14 kernel
+// launches per residue, for every sequence) with: one device-resident profile built once
+// (kernel-layout emission table + per-length transition table), and one persistent kernel
+// launch per batch.  Status codes are returned, never printed-and-continued (:198-203).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "msv.h"
+#include "msv_kernel.h"
+
+namespace {
+
+constexpr uint32_t kDefaultMaxLength = 131072;
+constexpr uint32_t kOrderBins = 1u << 16;
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// MSV_HMM::init_transitions_depend_on_seq (MSV_HMM.cpp:59-64) for every length < n, with the
+// host's logf (never a device logf, so the per-sequence constants are the reference's bits).
+const std::vector<float2>& host_length_table(uint32_t n) {
+    static std::mutex mu;
+    static std::vector<float2> table;
+    std::lock_guard<std::mutex> lock(mu);
+    if (table.size() < n) {
+        const size_t old = table.size();
+        table.resize(n);
+        for (size_t L = old; L < n; ++L) {
+            float loop, move;
+            msv_sequence_transitions(L, &loop, &move);
+            table[L] = make_float2(loop, move);
+        }
+    }
+    return table;
+}
+
+template <typename T>
+hipError_t ensure(T*& p, size_t& cap, size_t need) {
+    if (need <= cap && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t n = std::max<size_t>(need, 1);
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), n * sizeof(T));
+    if (e == hipSuccess) cap = n;
+    return e;
+}
+
+msv_status hip_status(hipError_t e) {
+    if (e == hipSuccess) return MSV_OK;
+    if (e == hipErrorOutOfMemory) return MSV_ERR_OUT_OF_MEMORY;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return MSV_ERR_NO_DEVICE;
+    return MSV_ERR_HIP;
+}
+
+#define MSV_HIP(call)                                    \
+    do {                                                 \
+        hipError_t e_ = (call);                          \
+        if (e_ != hipSuccess) return hip_status(e_);     \
+    } while (0)
+
+// Estimated issue cost of one row for one sequence: 2.5 VALU per state-slot plus the per-row
+// specials/reduction, times the lanes a sequence occupies.
+double variant_cost(const msvk::Variant& v) { return (2.5 * v.S + 26.0) * v.G * (v.big ? 1.6 : 1.0); }
+
+const msvk::Variant* pick_variant(uint32_t states) {
+    int count = 0;
+    const msvk::Variant* all = msvk::variants(&count);
+    const msvk::Variant* best = nullptr;
+    for (int i = 0; i < count; ++i) {
+        const msvk::Variant& v = all[i];
+        if (static_cast<uint32_t>(v.G * v.S) < states) continue;
+        if (!best || variant_cost(v) < variant_cost(*best)) best = &v;
+    }
+    return best;
+}
+
+}  // namespace
+
+struct msv_profile {
+    int device = 0;
+    uint32_t model_length = 0;  // LENG + 1
+    const msvk::Variant* v = nullptr;
+    float tr_B_Mk = 0, tr_E_C = 0, tr_E_J = 0;
+    float4* d_etab = nullptr;
+    float2* d_lentab = nullptr;
+    uint32_t lentab_n = 0;
+    uint32_t* d_words = nullptr;  // [0] dequeue counter, [1] sticky error bits
+    uint32_t* d_hist = nullptr;   // longest-first counting-sort scratch
+    uint8_t* d_dummy = nullptr;   // a readable residue byte for batches with no residues
+    hipStream_t stream = nullptr;
+    int blocks = 0;               // persistent grid size
+    int groups_per_block = 0;
+    // host-API staging
+    uint8_t* d_res = nullptr;
+    size_t d_res_cap = 0;
+    uint64_t* d_off = nullptr;
+    size_t d_off_cap = 0;
+    float* d_scores = nullptr;
+    size_t d_scores_cap = 0;
+};
+
+extern "C" {
+
+const char* msv_status_string(msv_status s) {
+    switch (s) {
+        case MSV_OK: return "MSV_OK";
+        case MSV_ERR_INVALID_ARGUMENT: return "MSV_ERR_INVALID_ARGUMENT";
+        case MSV_ERR_IO: return "MSV_ERR_IO";
+        case MSV_ERR_PARSE: return "MSV_ERR_PARSE";
+        case MSV_ERR_BAD_RESIDUE: return "MSV_ERR_BAD_RESIDUE";
+        case MSV_ERR_SEQUENCE_TOO_LONG: return "MSV_ERR_SEQUENCE_TOO_LONG";
+        case MSV_ERR_UNSUPPORTED_MODEL: return "MSV_ERR_UNSUPPORTED_MODEL";
+        case MSV_ERR_NO_DEVICE: return "MSV_ERR_NO_DEVICE";
+        case MSV_ERR_HIP: return "MSV_ERR_HIP";
+        case MSV_ERR_OUT_OF_MEMORY: return "MSV_ERR_OUT_OF_MEMORY";
+    }
+    return "MSV_ERR_UNKNOWN";
+}
+
+const char* msv_version(void) { return "msv-mi355x 0.1.0 (gfx950)"; }
+
+msv_status msv_device_count(int* count) {
+    if (!count) return MSV_ERR_INVALID_ARGUMENT;
+    *count = 0;
+    hipError_t e = hipGetDeviceCount(count);
+    if (e != hipSuccess) {
+        *count = 0;
+        return MSV_ERR_NO_DEVICE;
+    }
+    return MSV_OK;
+}
+
+void msv_sequence_transitions(uint64_t L, float* tr_loop, float* tr_move) {
+    // MSV_HMM.cpp:59-64: size = seq.size() - 1; log(size / float(size + 3)), log(3 / float(size + 3))
+    const uint64_t size = L;
+    *tr_loop = std::log(size / static_cast<float>(size + 3));
+    *tr_move = std::log(3 / static_cast<float>(size + 3));
+}
+
+msv_status msv_hmm_msv_scores(const msv_hmm* hmm, float* emission_scores, float* tr_B_Mk, float* tr_E_C,
+                              float* tr_E_J) {
+    if (!hmm || !emission_scores || !tr_B_Mk || !tr_E_C || !tr_E_J) return MSV_ERR_INVALID_ARGUMENT;
+    // MSV_HMM::MSV_HMM, MSV_HMM.cpp:35-57
+    static constexpr float bg[20] = {0.0787945f, 0.0151600f, 0.0535222f, 0.0668298f, 0.0397062f,
+                                     0.0695071f, 0.0229198f, 0.0590092f, 0.0594422f, 0.0963728f,
+                                     0.0237718f, 0.0414386f, 0.0482904f, 0.0395639f, 0.0540978f,
+                                     0.0683364f, 0.0540687f, 0.0673417f, 0.0114135f, 0.0304133f};
+    const size_t M = msv_hmm_model_length(hmm);
+    const float* match = msv_hmm_match_emissions(hmm);
+    for (size_t i = 0; i < M; ++i)
+        for (size_t j = 0; j < 20; ++j) emission_scores[j * M + i] = std::log(match[i * 20 + j] / bg[j]);
+    constexpr float nu = 2.0f;
+    *tr_B_Mk = std::log(2.0f / static_cast<float>(M * (M + 1)));
+    *tr_E_C = std::log((nu - 1.0f) / nu);
+    *tr_E_J = std::log(1.0f / nu);
+    return MSV_OK;
+}
+
+void msv_profile_destroy(msv_profile* p) {
+    if (!p) return;
+    DeviceGuard g(p->device);
+    (void)hipFree(p->d_etab);
+    (void)hipFree(p->d_lentab);
+    (void)hipFree(p->d_words);
+    (void)hipFree(p->d_hist);
+    (void)hipFree(p->d_dummy);
+    (void)hipFree(p->d_res);
+    (void)hipFree(p->d_off);
+    (void)hipFree(p->d_scores);
+    if (p->stream) (void)hipStreamDestroy(p->stream);
+    delete p;
+}
+
+msv_status msv_profile_reserve_length(msv_profile* p, uint64_t max_length) {
+    if (!p) return MSV_ERR_INVALID_ARGUMENT;
+    if (max_length >= (1ull << 31)) return MSV_ERR_SEQUENCE_TOO_LONG;
+    const uint32_t need = static_cast<uint32_t>(max_length) + 1;
+    if (need <= p->lentab_n) return MSV_OK;
+    DeviceGuard g(p->device);
+    if (!g.ok) return MSV_ERR_NO_DEVICE;
+    const uint32_t n = std::max(need, p->lentab_n * 2);
+    const std::vector<float2>& host = host_length_table(n);
+    float2* d = nullptr;
+    MSV_HIP(hipMalloc(reinterpret_cast<void**>(&d), n * sizeof(float2)));
+    hipError_t e = hipMemcpy(d, host.data(), n * sizeof(float2), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return hip_status(e);
+    }
+    // the old table may still be read by an in-flight launch on the profile's stream
+    if (p->d_lentab) {
+        (void)hipStreamSynchronize(p->stream);
+        (void)hipFree(p->d_lentab);
+    }
+    p->d_lentab = d;
+    p->lentab_n = n;
+    return MSV_OK;
+}
+
+msv_status msv_profile_create(int device, const float* emission_scores, uint32_t model_length, float tr_B_Mk,
+                              float tr_E_C, float tr_E_J, msv_profile** out) {
+    if (!emission_scores || !out || model_length < 2) return MSV_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MSV_ERR_NO_DEVICE;
+    if (device < 0 || device >= ndev) return MSV_ERR_NO_DEVICE;
+    const uint32_t R = model_length - 1;  // real match states (MSV_HMM.cpp:285)
+    const msvk::Variant* v = pick_variant(R);
+    if (!v) return MSV_ERR_UNSUPPORTED_MODEL;
+
+    DeviceGuard g(device);
+    if (!g.ok) return MSV_ERR_NO_DEVICE;
+    auto* p = new (std::nothrow) msv_profile;
+    if (!p) return MSV_ERR_OUT_OF_MEMORY;
+    p->device = device;
+    p->model_length = model_length;
+    p->v = v;
+    p->tr_B_Mk = tr_B_Mk;
+    p->tr_E_C = tr_E_C;
+    p->tr_E_J = tr_E_J;
+
+    // Kernel layout: [row r][chunk c][lane gl] float4 = e[r][gl*S + 4c + 1 .. +4]; states beyond
+    // LENG are -inf (never win a max); row 20 is the +inf poison row for codes >= 20.
+    const int G = v->G, S = v->S, C4 = S / 4;
+    std::vector<float> tab(static_cast<size_t>(msvk::kTableRows) * C4 * G * 4);
+    const float ninf = -std::numeric_limits<float>::infinity();
+    const float pinf = std::numeric_limits<float>::infinity();
+    for (int r = 0; r < msvk::kTableRows; ++r)
+        for (int c = 0; c < C4; ++c)
+            for (int gl = 0; gl < G; ++gl)
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t j = static_cast<uint32_t>(gl * S + 4 * c + q + 1);  // match state 1..
+                    float val;
+                    if (r == msvk::kPoisonRow) val = pinf;
+                    else val = (j <= R) ? emission_scores[static_cast<size_t>(r) * model_length + j] : ninf;
+                    tab[((static_cast<size_t>(r) * C4 + c) * G + gl) * 4 + q] = val;
+                }
+
+    auto fail = [&](hipError_t e) {
+        msv_profile_destroy(p);
+        return hip_status(e);
+    };
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_etab), tab.size() * sizeof(float))) != hipSuccess) return fail(e);
+    if ((e = hipMemcpy(p->d_etab, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(e);
+    if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_words), 4 * sizeof(uint32_t))) != hipSuccess) return fail(e);
+    if ((e = hipMemset(p->d_words, 0, 4 * sizeof(uint32_t))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_dummy), 64)) != hipSuccess) return fail(e);
+    if ((e = hipMemset(p->d_dummy, 0, 64)) != hipSuccess) return fail(e);
+
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return fail(e);
+    int per_cu = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(v->fn), v->waves * 64, 0);
+    if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    p->blocks = prop.multiProcessorCount * per_cu;
+    p->groups_per_block = v->waves * (64 / G);
+
+    msv_status s = msv_profile_reserve_length(p, kDefaultMaxLength - 1);
+    if (s != MSV_OK) {
+        msv_profile_destroy(p);
+        return s;
+    }
+    *out = p;
+    return MSV_OK;
+}
+
+msv_status msv_profile_create_from_hmm(int device, const msv_hmm* hmm, msv_profile** out) {
+    if (!hmm || !out) return MSV_ERR_INVALID_ARGUMENT;
+    const size_t M = msv_hmm_model_length(hmm);
+    std::vector<float> es(M * 20);
+    float b, c, j;
+    msv_status s = msv_hmm_msv_scores(hmm, es.data(), &b, &c, &j);
+    if (s != MSV_OK) return s;
+    return msv_profile_create(device, es.data(), static_cast<uint32_t>(M), b, c, j, out);
+}
+
+msv_status msv_profile_describe(const msv_profile* p, msv_kernel_info* out) {
+    if (!p || !out) return MSV_ERR_INVALID_ARGUMENT;
+    std::memset(out, 0, sizeof(*out));
+    out->model_length = p->model_length;
+    out->lanes_per_group = static_cast<uint32_t>(p->v->G);
+    out->states_per_lane = static_cast<uint32_t>(p->v->S);
+    out->waves_per_block = static_cast<uint32_t>(p->v->waves);
+    out->lds_rows = static_cast<uint32_t>(p->v->lds_rows);
+    out->lds_bytes = static_cast<uint32_t>(p->v->lds_rows * p->v->G * p->v->S * 4);
+    out->blocks = static_cast<uint32_t>(p->blocks);
+    out->max_length = p->lentab_n ? p->lentab_n - 1 : 0;
+    out->device = p->device;
+    std::snprintf(out->variant, sizeof(out->variant), "%s", p->v->name);
+    return MSV_OK;
+}
+
+msv_status msv_score_batch_device(msv_profile* p, const uint8_t* d_residues, uint64_t residues_len,
+                                  const uint64_t* d_offsets, uint64_t n, const uint32_t* d_order, float* d_scores,
+                                  void* stream) {
+    if (!p) return MSV_ERR_INVALID_ARGUMENT;
+    if (n == 0) return MSV_OK;
+    if (!d_offsets || !d_scores || (residues_len && !d_residues)) return MSV_ERR_INVALID_ARGUMENT;
+    if (residues_len >= (1ull << 32) || n >= (1ull << 32) - (1ull << 24)) return MSV_ERR_INVALID_ARGUMENT;
+    DeviceGuard g(p->device);
+    if (!g.ok) return MSV_ERR_NO_DEVICE;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p->stream;
+
+    msvk::KernelArgs a{};
+    a.etab = p->d_etab;
+    a.residues = residues_len ? d_residues : p->d_dummy;
+    a.offsets = d_offsets;
+    a.order = d_order;
+    a.lentab = p->d_lentab;
+    a.scores = d_scores;
+    a.counter = p->d_words;
+    a.errors = p->d_words + 1;
+    a.n = n;
+    a.lentab_n = p->lentab_n;
+    a.tr_B_Mk = p->tr_B_Mk;
+    a.tr_E_C = p->tr_E_C;
+    a.tr_E_J = p->tr_E_J;
+
+    const uint64_t want = (n + p->groups_per_block - 1) / p->groups_per_block;
+    const int blocks = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(p->blocks), want));
+    MSV_HIP(hipMemsetAsync(p->d_words, 0, sizeof(uint32_t), st));
+    MSV_HIP(msvk::launch_variant(*p->v, dim3(blocks), a, st));
+    return MSV_OK;
+}
+
+msv_status msv_profile_check(msv_profile* p, void* stream) {
+    if (!p) return MSV_ERR_INVALID_ARGUMENT;
+    DeviceGuard g(p->device);
+    if (!g.ok) return MSV_ERR_NO_DEVICE;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p->stream;
+    uint32_t err = 0;
+    MSV_HIP(hipMemcpyAsync(&err, p->d_words + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    MSV_HIP(hipStreamSynchronize(st));
+    if (err) MSV_HIP(hipMemsetAsync(p->d_words + 1, 0, sizeof(uint32_t), st));
+    MSV_HIP(hipStreamSynchronize(st));
+    if (err & msvk::kErrBadResidue) return MSV_ERR_BAD_RESIDUE;
+    if (err & msvk::kErrTooLong) return MSV_ERR_SEQUENCE_TOO_LONG;
+    return MSV_OK;
+}
+
+msv_status msv_order_longest_first(msv_profile* p, const uint64_t* d_offsets, uint64_t n, uint32_t* d_order,
+                                   void* stream) {
+    if (!p || (n && (!d_offsets || !d_order))) return MSV_ERR_INVALID_ARGUMENT;
+    if (n == 0) return MSV_OK;
+    DeviceGuard g(p->device);
+    if (!g.ok) return MSV_ERR_NO_DEVICE;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p->stream;
+    if (!p->d_hist) MSV_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_hist), kOrderBins * sizeof(uint32_t)));
+    MSV_HIP(msvk::launch_order(d_offsets, n, p->d_hist, kOrderBins, d_order, st));
+    return MSV_OK;
+}
+
+msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
+                           float* scores, void* stream) {
+    if (!p || (n && (!offsets || !scores))) return MSV_ERR_INVALID_ARGUMENT;
+    if (n == 0) return MSV_OK;
+    // Validate the CSR on the host (cheap, O(n)) and find the longest sequence.
+    uint64_t maxL = 0;
+    for (uint64_t s = 0; s < n; ++s) {
+        if (offsets[s + 1] < offsets[s]) return MSV_ERR_INVALID_ARGUMENT;
+        maxL = std::max<uint64_t>(maxL, offsets[s + 1] - offsets[s]);
+    }
+    if (offsets[n] > offsets[0] && !residues) return MSV_ERR_INVALID_ARGUMENT;
+    msv_status s = msv_profile_reserve_length(p, maxL);
+    if (s != MSV_OK) return s;
+
+    DeviceGuard g(p->device);
+    if (!g.ok) return MSV_ERR_NO_DEVICE;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p->stream;
+
+    // Chunk so that every launch addresses < 2^32 residue bytes.
+    constexpr uint64_t kChunkBytes = (1ull << 32) - (1ull << 20);
+    uint64_t first = 0;
+    while (first < n) {
+        uint64_t last = first + 1;
+        while (last < n && offsets[last + 1] - offsets[first] < kChunkBytes) ++last;
+        if (offsets[last] - offsets[first] >= kChunkBytes) return MSV_ERR_SEQUENCE_TOO_LONG;
+        const uint64_t cn = last - first;
+        const uint64_t base = offsets[first];
+        const uint64_t bytes = offsets[last] - base;
+        MSV_HIP(ensure(p->d_res, p->d_res_cap, bytes));
+        MSV_HIP(ensure(p->d_off, p->d_off_cap, cn + 1));
+        MSV_HIP(ensure(p->d_scores, p->d_scores_cap, cn));
+        std::vector<uint64_t> rebased(cn + 1);
+        for (uint64_t k = 0; k <= cn; ++k) rebased[k] = offsets[first + k] - base;
+        if (bytes) MSV_HIP(hipMemcpyAsync(p->d_res, residues + base, bytes, hipMemcpyHostToDevice, st));
+        MSV_HIP(hipMemcpyAsync(p->d_off, rebased.data(), (cn + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+        s = msv_score_batch_device(p, p->d_res, bytes, p->d_off, cn, nullptr, p->d_scores, st);
+        if (s != MSV_OK) return s;
+        MSV_HIP(hipMemcpyAsync(scores + first, p->d_scores, cn * sizeof(float), hipMemcpyDeviceToHost, st));
+        MSV_HIP(hipStreamSynchronize(st));  // `rebased` is pageable host memory read by the copy
+        s = msv_profile_check(p, st);
+        if (s != MSV_OK) return s;
+        first = last;
+    }
+    return MSV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,88 @@
+// msv_hmm.cpp -- MSV_HMM, the reference's class surface (algorithms/MSV_HMM.hpp:17-44), on the
+// C-ABI device path.  The host precompute is the reference's (MSV_HMM.cpp:35-57, host libm);
+// every score is computed by the fused gfx950 kernel.
+#include <cmath>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "msv.h"
+#include "msv_hmm.hpp"
+
+namespace {
+
+void check(msv_status s, const char* what) {
+    if (s != MSV_OK) throw msv_error(s, std::string(what) + ": " + msv_status_string(s));
+}
+
+// background_frequencies, MSV_HMM.cpp:21-27
+constexpr float kBackground[NUM_OF_AMINO_ACIDS] = {
+    0.0787945f, 0.0151600f, 0.0535222f, 0.0668298f, 0.0397062f, 0.0695071f, 0.0229198f,
+    0.0590092f, 0.0594422f, 0.0963728f, 0.0237718f, 0.0414386f, 0.0482904f, 0.0395639f,
+    0.0540978f, 0.0683364f, 0.0540687f, 0.0673417f, 0.0114135f, 0.0304133f};
+
+}  // namespace
+
+MSV_HMM::MSV_HMM(const Profile_HMM& base_hmm, int device) : model_length_(base_hmm.model_length) {
+    // MSV_HMM.cpp:38-45: [20][model_length] log-odds, column 0 = log(0) = -inf
+    emission_scores_.assign(NUM_OF_AMINO_ACIDS * model_length_, 0.f);
+    for (size_t i = 0; i < model_length_; ++i)
+        for (size_t j = 0; j < NUM_OF_AMINO_ACIDS; ++j)
+            emission_scores_[j * model_length_ + i] = std::log(base_hmm.match_emissions[i][j] / kBackground[j]);
+    constexpr float nu = 2.0;  // MSV_HMM.cpp:49
+    tr_B_Mk_ = std::log(2.0f / static_cast<float>(base_hmm.model_length * (base_hmm.model_length + 1)));
+    tr_E_C_ = std::log((nu - 1.0f) / nu);
+    tr_E_J_ = std::log(1.0f / nu);
+    check(msv_profile_create(device, emission_scores_.data(), static_cast<uint32_t>(model_length_), tr_B_Mk_,
+                             tr_E_C_, tr_E_J_, &profile_),
+          "msv_profile_create");
+}
+
+MSV_HMM::~MSV_HMM() { msv_profile_destroy(profile_); }
+
+MSV_HMM::MSV_HMM(MSV_HMM&& o) noexcept
+    : model_length_(o.model_length_),
+      emission_scores_(std::move(o.emission_scores_)),
+      tr_B_Mk_(o.tr_B_Mk_),
+      tr_E_C_(o.tr_E_C_),
+      tr_E_J_(o.tr_E_J_),
+      profile_(std::exchange(o.profile_, nullptr)) {}
+
+MSV_HMM& MSV_HMM::operator=(MSV_HMM&& o) noexcept {
+    if (this != &o) {
+        msv_profile_destroy(profile_);
+        model_length_ = o.model_length_;
+        emission_scores_ = std::move(o.emission_scores_);
+        tr_B_Mk_ = o.tr_B_Mk_;
+        tr_E_C_ = o.tr_E_C_;
+        tr_E_J_ = o.tr_E_J_;
+        profile_ = std::exchange(o.profile_, nullptr);
+    }
+    return *this;
+}
+
+Log_score MSV_HMM::run_on_sequence(const Protein_sequence& seq) { return score_batch(Protein_sequences{seq})[0]; }
+
+Log_score MSV_HMM::parallel_run_on_sequence(const Protein_sequence& seq, bool /*should_specialize*/) {
+    // The reference's should_specialize bakes sizes and transition constants into the OpenCL
+    // program through -D defines (MSV_HMM.cpp:322-337); here the sizes are always compile-time
+    // template parameters of the kernel and the constants are exact floats, so both settings
+    // run the same specialised kernel and return the same (reference-exact) score.
+    return run_on_sequence(seq);
+}
+
+std::vector<Log_score> MSV_HMM::score_batch(const Protein_sequences& seqs) {
+    return score_batch(Packed_sequences::pack(seqs));
+}
+
+std::vector<Log_score> MSV_HMM::score_batch(const Packed_sequences& packed) {
+    return score_batch(packed.codes.data(), packed.offsets.data(), packed.size());
+}
+
+std::vector<Log_score> MSV_HMM::score_batch(const uint8_t* codes, const uint64_t* offsets, size_t n) {
+    std::vector<Log_score> out(n);
+    const msv_status s = msv_score_batch(profile_, codes, offsets, n, out.data(), nullptr);
+    if (s == MSV_ERR_BAD_RESIDUE) throw std::out_of_range("residue outside the 20 amino acids");
+    check(s, "msv_score_batch");
+    return out;
+}

@@ -1,0 +1,50 @@
+// msv_kernel.h -- device-side interface shared by msv_kernel.hip and the C-ABI layer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace msvk {
+
+constexpr int kAminoAcids = 20;
+constexpr int kPoisonRow = 20;   // codes >= 20 are clamped here; the row is +inf -> score +inf -> error
+constexpr int kTableRows = 21;   // 20 residues + poison row
+constexpr int kLdsLimit = 163840;
+
+constexpr uint32_t kErrBadResidue = 1u;
+constexpr uint32_t kErrTooLong = 2u;
+
+// Residue rows of the [row][chunk][lane] float4 table that fit the 160 KiB LDS of one CU.
+constexpr int lds_rows_for(int G, int S) {
+    return (kLdsLimit / (G * S * 4)) >= kTableRows ? kTableRows : (kLdsLimit / (G * S * 4));
+}
+
+struct KernelArgs {
+    const float4* etab;        // [21][S/4][G] float4, global copy of the kernel-layout table
+    const uint8_t* residues;   // CSR residue codes
+    const uint64_t* offsets;   // n + 1
+    const uint32_t* order;     // optional dequeue permutation (n) or nullptr
+    const float2* lentab;      // [lentab_n] {tr_loop, tr_move} indexed by sequence length
+    float* scores;             // n
+    uint32_t* counter;         // dequeue head, zeroed before each launch
+    uint32_t* errors;          // sticky error bits
+    uint64_t n;
+    uint32_t lentab_n;
+    float tr_B_Mk, tr_E_C, tr_E_J;
+};
+
+struct Variant {
+    int G, S, waves;
+    int lds_rows;
+    bool big;
+    const void* fn;
+    const char* name;
+};
+
+const Variant* variants(int* count);
+hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, hipStream_t stream);
+hipError_t launch_order(const uint64_t* offsets, uint64_t n, uint32_t* scratch_hist, uint32_t nbins, uint32_t* order,
+                        hipStream_t stream);
+
+}  // namespace msvk

@@ -1,0 +1,335 @@
+// msv_kernel.hip -- the MSV hot path as ONE fused CDNA4 (gfx950) kernel per batch.
+//
+// Replaces MSV_HMM::parallel_run_on_sequence (algorithms/MSV_HMM.cpp:269-430) and its six
+// OpenCL kernels (algorithms/MSV_kernels.cl:1-65, MSV_spec_kernels.cl:1-50): the reference
+// launches 9-14 kernels PER RESIDUE for ONE sequence; here one persistent launch scores a whole
+// batch of sequences against one profile, with every DP row kept on-chip.
+//
+// Recurrence (bit-exact restatement of MSV_HMM::run_on_sequence, MSV_HMM.cpp:100-112), for a
+// residue r at row i:
+//     Bt   = B' + tr_B_Mk
+//     M_j  = e[r][j] + max(M'_{j-1}, Bt)          j = 1..LENG, M'_0 = -inf
+//     E    = max_j M_j
+//     J    = max(J' + loop, E + tEJ);  C = max(C' + loop, E + tEC)
+//     N    = N' + loop;                B = max(N + move, J + move) == max(N, J) + move
+// score = C_L + move.  Only IEEE adds and maxes: max is exact and fl() is monotone, so
+// max(N+move, J+move) == fl(max(N,J) + move) bit for bit; no multiply exists, so no contraction.
+//
+// Mapping (MI355X-first, not a translation of the OpenCL NDRange-per-residue):
+//   * A "group" of G lanes (G = 16 or 32) owns ONE sequence; lane gl holds the S consecutive
+//     match states gl*S+1 .. gl*S+S of the DP row in VGPRs (float M[S]).  A 64-lane wave runs
+//     64/G independent sequences.
+//   * The j-1 neighbour crosses a lane boundary once per row: one DPP row_shr:1 (+ row_bcast:15
+//     for G=32) moves M[S-1] to the next lane; lane 0 of a group reads M_0 = -inf.
+//   * E: per-lane max3 tree, then a DPP butterfly (quad_perm, row_half_mirror, row_mirror) and a
+//     v_permlane16_swap for G=32 -- no LDS, no barrier.
+//   * The 20 x (G*S) fp32 emission table (+1 poison row of +inf for codes >= 20) lives in LDS,
+//     laid out [residue][chunk][lane] float4 so every ds_read_b128 of a group is contiguous.
+//     One workgroup per CU shares the table across all its waves.  Profiles whose table does not
+//     fit the 160 KiB LDS ("BIG", LENG > ~1950) keep the rows that fit in LDS and read the rest
+//     through generic (flat) loads from L2.
+//   * Persistent grid: every group dequeues sequences from a device counter (prefetched one
+//     sequence ahead, one atomic per sequence), so long and short sequences load-balance with no
+//     host scheduling; a group that reaches the end of its sequence writes the score and starts
+//     the next one in place.
+//   * The residue stream is read one byte per row per group (global_load_ubyte, L1/L2-served,
+//     two rows of prefetch); the per-length transition constants come from a host-computed table
+//     (host logf, so scores never depend on a device logf).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "msv_kernel.h"
+
+namespace msvk {
+
+namespace {
+
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF>
+__device__ __forceinline__ float dpp(float old, float src) {
+    // bound_ctrl = false: a lane whose DPP source is invalid keeps `old`.
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), CTRL, ROW_MASK,
+                                                      BANK_MASK, false));
+}
+
+constexpr int DPP_QUAD_1032 = 0xB1;    // quad_perm:[1,0,3,2]
+constexpr int DPP_QUAD_2301 = 0x4E;    // quad_perm:[2,3,0,1]
+constexpr int DPP_ROW_SHR1 = 0x111;    // row_shr:1
+constexpr int DPP_ROW_MIRROR = 0x140;  // row_mirror
+constexpr int DPP_ROW_HMIRROR = 0x141; // row_half_mirror
+constexpr int DPP_ROW_BCAST15 = 0x142; // row_bcast:15
+
+// M_{j-1} for the first state of each lane: the last state of the previous lane of the same
+// group; -inf (the dummy M0 column, MSV_HMM.cpp:86) for the first lane of a group.
+template <int G>
+__device__ __forceinline__ float shift_in(float last, float ninf) {
+    if constexpr (G == 16) {
+        return dpp<DPP_ROW_SHR1>(ninf, last);
+    } else {
+        static_assert(G == 32, "G must be 16 or 32");
+        // rows 1 and 3 first receive lane 15 of rows 0 and 2; row_shr:1 then fills every lane
+        // except the first of each row, which keeps that broadcast (or -inf for rows 0 and 2).
+        float v = dpp<DPP_ROW_BCAST15, 0xA>(ninf, last);
+        return dpp<DPP_ROW_SHR1>(v, last);
+    }
+}
+
+// In-row permutation (every source lane valid): lets the DPP combiner fold it into v_max_f32_dpp.
+template <int CTRL>
+__device__ __forceinline__ float dpp_perm(float src) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(src), CTRL, 0xF, 0xF, true));
+}
+
+// Max over the G lanes of a group, result in every lane of the group.
+template <int G>
+__device__ __forceinline__ float group_max(float x) {
+    x = fmaxf(x, dpp_perm<DPP_QUAD_1032>(x));
+    x = fmaxf(x, dpp_perm<DPP_QUAD_2301>(x));
+    x = fmaxf(x, dpp_perm<DPP_ROW_HMIRROR>(x));
+    x = fmaxf(x, dpp_perm<DPP_ROW_MIRROR>(x));
+    if constexpr (G == 32) {
+        auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        x = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+    }
+    return x;
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t group_bcast(uint32_t v, int lane) {
+    return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute((lane & ~(G - 1)) << 2, static_cast<int>(v)));
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t group_dequeue(uint32_t* counter, bool leader, int lane) {
+    uint32_t v = 0;
+    if (leader) v = atomicAdd(counter, 1u);
+    return group_bcast<G>(v, lane);
+}
+
+}  // namespace
+
+template <int G, int S, int WAVES, bool BIG>
+__global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs a) {
+    static_assert(S % 4 == 0, "S must be a multiple of 4 (float4 chunks)");
+    constexpr int C4 = S / 4;
+    constexpr int ROW_F4 = C4 * G;  // float4 per residue row
+    constexpr int LDS_ROWS = lds_rows_for(G, S);
+    static_assert(BIG == (LDS_ROWS < kTableRows), "BIG <=> table does not fit LDS");
+    __shared__ float4 tab[LDS_ROWS * ROW_F4];
+
+    const float NINF = -__builtin_inff();
+    const int lane = threadIdx.x & 63;
+    const int gl = lane & (G - 1);
+    const bool leader = gl == 0;
+
+    // Stage the emission table (already in kernel layout) into LDS once per workgroup.
+    for (int i = threadIdx.x; i < LDS_ROWS * ROW_F4; i += WAVES * 64) tab[i] = a.etab[i];
+    __syncthreads();
+
+    const uint8_t* __restrict__ res = a.residues;
+    const float trBMk = a.tr_B_Mk, tEC = a.tr_E_C, tEJ = a.tr_E_J;
+
+    float M[S];
+    float J = NINF, C = NINF, N = 0.f, B = 0.f, loop = 0.f, move = 0.f;
+    uint32_t pos = 0, endpos = 0, rows_left = 0xFFFFFFFFu, seq = 0;
+    bool active = false;
+#pragma unroll
+    for (int k = 0; k < S; ++k) M[k] = NINF;
+
+    uint32_t cur = group_dequeue<G>(a.counter, leader, lane);
+    uint32_t nxt = group_dequeue<G>(a.counter, leader, lane);
+
+    // Start the next non-empty sequence of this group (or retire the group).
+    auto begin = [&]() {
+        for (;;) {
+            if (cur >= a.n) {
+                active = false;
+                pos = 0;
+                endpos = 0;
+                rows_left = 0xFFFFFFFFu;
+                return;
+            }
+            const uint32_t s = a.order ? a.order[cur] : cur;
+            const uint64_t o0 = a.offsets[s], o1 = a.offsets[s + 1];
+            const uint64_t L = o1 - o0;
+            cur = nxt;
+            nxt = group_dequeue<G>(a.counter, leader, lane);
+            if (L == 0) {  // empty record: the DP loop never runs, C_0 = -inf (MSV_HMM.cpp:86,112)
+                if (leader) a.scores[s] = NINF;
+                continue;
+            }
+            if (L >= a.lentab_n) {
+                if (leader) {
+                    a.scores[s] = __uint_as_float(0x7fc00000u);  // quiet NaN bits
+                    atomicOr(a.errors, kErrTooLong);
+                }
+                continue;
+            }
+            const float2 lm = a.lentab[L];
+            loop = lm.x;
+            move = lm.y;
+            seq = s;
+            pos = static_cast<uint32_t>(o0);
+            endpos = static_cast<uint32_t>(o1 - 1);
+            rows_left = static_cast<uint32_t>(L);
+#pragma unroll
+            for (int k = 0; k < S; ++k) M[k] = NINF;
+            J = NINF;
+            C = NINF;
+            N = 0.f;    // dp[0][N] = 0      (MSV_HMM.cpp:96)
+            B = move;   // dp[0][B] = tr_move (MSV_HMM.cpp:97)
+            active = true;
+            return;
+        }
+    };
+
+    begin();
+    uint32_t r0 = res[pos];
+    uint32_t r1 = res[min(pos + 1, endpos)];
+
+    while (__any(active)) {
+        const uint32_t r2 = res[min(pos + 2, endpos)];
+        const uint32_t rr = min(r0, static_cast<uint32_t>(kPoisonRow));
+
+        float4 e[C4];
+        if constexpr (!BIG) {
+            const float4* ep = &tab[rr * ROW_F4 + gl];
+#pragma unroll
+            for (int c = 0; c < C4; ++c) e[c] = ep[c * G];
+        } else {
+            const float4* ep = (rr < static_cast<uint32_t>(LDS_ROWS)) ? &tab[rr * ROW_F4 + gl]
+                                                                      : &a.etab[rr * ROW_F4 + gl];
+#pragma unroll
+            for (int c = 0; c < C4; ++c) e[c] = ep[c * G];
+        }
+
+        const float Bt = B + trBMk;
+        const float nbr = shift_in<G>(M[S - 1], NINF);
+
+        // Update in place from the highest state down, so M[k-1] is still the previous row.
+#pragma unroll
+        for (int k = S - 1; k >= 1; --k) {
+            const float4 ev = e[k >> 2];
+            const float ek = (k & 3) == 0 ? ev.x : (k & 3) == 1 ? ev.y : (k & 3) == 2 ? ev.z : ev.w;
+            M[k] = ek + fmaxf(M[k - 1], Bt);
+        }
+        M[0] = e[0].x + fmaxf(nbr, Bt);
+
+        // E = max_j M_j : four independent max3 chains, then the group butterfly.
+        float p0 = M[0], p1 = M[1], p2 = M[2], p3 = M[3];
+#pragma unroll
+        for (int k = 4; k < S; k += 4) {
+            p0 = fmaxf(p0, M[k]);
+            p1 = fmaxf(p1, M[k + 1]);
+            p2 = fmaxf(p2, M[k + 2]);
+            p3 = fmaxf(p3, M[k + 3]);
+        }
+        const float E = group_max<G>(fmaxf(fmaxf(p0, p1), fmaxf(p2, p3)));
+
+        J = fmaxf(J + loop, E + tEJ);
+        C = fmaxf(C + loop, E + tEC);
+        N = N + loop;
+        B = fmaxf(N, J) + move;
+
+        ++pos;
+        --rows_left;
+        r0 = r1;
+        r1 = r2;
+        if (rows_left == 0) {
+            const float sc = C + move;  // dp.back()[C] + tr_move (MSV_HMM.cpp:112)
+            if (leader) {
+                a.scores[seq] = sc;
+                if (!(sc <= 3.402823466e38f)) atomicOr(a.errors, kErrBadResidue);  // poison row hit
+            }
+            begin();
+            r0 = res[pos];
+            r1 = res[min(pos + 1, endpos)];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Longest-first dequeue order (counting sort on the device): hist -> scan -> scatter.
+// ------------------------------------------------------------------------------------------------
+__global__ void order_hist_kernel(const uint64_t* __restrict__ offsets, uint64_t n, uint32_t* __restrict__ hist,
+                                  uint32_t nbins) {
+    for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < n; s += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t L = offsets[s + 1] - offsets[s];
+        uint32_t b = L >= nbins ? nbins - 1 : static_cast<uint32_t>(L);
+        atomicAdd(&hist[nbins - 1 - b], 1u);  // descending length
+    }
+}
+
+__global__ void order_scan_kernel(uint32_t* __restrict__ hist, uint32_t nbins) {
+    // single block exclusive scan, in place (nbins is small: <= 1 << 16)
+    __shared__ uint32_t partial[1024];
+    const uint32_t t = threadIdx.x, T = blockDim.x;
+    const uint32_t per = (nbins + T - 1) / T;
+    const uint32_t lo = t * per, hi = min(nbins, lo + per);
+    uint32_t sum = 0;
+    for (uint32_t i = lo; i < hi; ++i) sum += hist[i];
+    partial[t] = sum;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t run = 0;
+        for (uint32_t i = 0; i < T; ++i) {
+            uint32_t v = partial[i];
+            partial[i] = run;
+            run += v;
+        }
+    }
+    __syncthreads();
+    uint32_t run = partial[t];
+    for (uint32_t i = lo; i < hi; ++i) {
+        uint32_t v = hist[i];
+        hist[i] = run;
+        run += v;
+    }
+}
+
+__global__ void order_scatter_kernel(const uint64_t* __restrict__ offsets, uint64_t n, uint32_t* __restrict__ cursor,
+                                     uint32_t nbins, uint32_t* __restrict__ order) {
+    for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < n; s += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t L = offsets[s + 1] - offsets[s];
+        uint32_t b = L >= nbins ? nbins - 1 : static_cast<uint32_t>(L);
+        uint32_t slot = atomicAdd(&cursor[nbins - 1 - b], 1u);
+        order[slot] = static_cast<uint32_t>(s);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Variant table: every compiled (G, S, WAVES) instantiation.  The host picks the one whose G*S
+// covers LENG with the least estimated cost (the analog of the reference's should_specialize,
+// which bakes sizes into the OpenCL program with -D defines, MSV_HMM.cpp:322-337).
+// ------------------------------------------------------------------------------------------------
+#define MSV_VARIANT(G_, S_, W_)                                                                             \
+    Variant{G_, S_, W_, lds_rows_for(G_, S_), lds_rows_for(G_, S_) < kTableRows,                            \
+            reinterpret_cast<const void*>(&msv_batch_kernel<G_, S_, W_, (lds_rows_for(G_, S_) < kTableRows)>), \
+            "msv_g" #G_ "_s" #S_ "_w" #W_}
+
+static const Variant kVariants[] = {
+#include "msv_variants.inc"
+};
+
+const Variant* variants(int* count) {
+    *count = static_cast<int>(sizeof(kVariants) / sizeof(kVariants[0]));
+    return kVariants;
+}
+
+hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, hipStream_t stream) {
+    void* params[] = {const_cast<KernelArgs*>(&args)};
+    return hipLaunchKernel(v.fn, grid, dim3(v.waves * 64), params, 0, stream);
+}
+
+hipError_t launch_order(const uint64_t* offsets, uint64_t n, uint32_t* scratch_hist, uint32_t nbins, uint32_t* order,
+                        hipStream_t stream) {
+    hipError_t e = hipMemsetAsync(scratch_hist, 0, nbins * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    const uint32_t blocks = static_cast<uint32_t>(n / 256 + 1 > 1024 ? 1024 : n / 256 + 1);
+    hipLaunchKernelGGL(order_hist_kernel, dim3(blocks), dim3(256), 0, stream, offsets, n, scratch_hist, nbins);
+    hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(1024), 0, stream, scratch_hist, nbins);
+    hipLaunchKernelGGL(order_scatter_kernel, dim3(blocks), dim3(256), 0, stream, offsets, n, scratch_hist, nbins, order);
+    return hipGetLastError();
+}
+
+}  // namespace msvk

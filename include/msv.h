@@ -1,0 +1,157 @@
+/*
+ * msv.h -- C-ABI of the MI355X-native MSV (Multiple Segment Viterbi) scoring engine.
+ *
+ * This is the drop-in boundary for the reference's single hot path, the class
+ * MSV_HMM (algorithms/MSV_HMM.hpp:17-44 of IvanTyulyandin/HMM_FASTA_Viterbi).  Plain C types
+ * only: no HIP, no torch, no C++ in the signatures.  Every entry point cites the reference
+ * interface it replaces.  All functions return an msv_status; nothing prints and continues
+ * (the reference's check_errors prints and continues, MSV_HMM.cpp:198-203).
+ *
+ * Ownership: the caller owns every buffer it passes; the library owns the device buffers held
+ * by an msv_profile.  One msv_profile may be used by one host thread at a time (the reference
+ * MSV_HMM is likewise not thread-safe, MSV_HMM.hpp:33-34); separate profiles are independent.
+ *
+ * Residues cross the boundary as codes 0..19 in the reference's alphabetical order
+ * A C D E F G H I K L M N P Q R S T V W Y (MSV_HMM.cpp:29-31), without the '#' sentinel that
+ * the reference prepends (FASTA_protein_sequences.cpp:19-20), in a CSR layout:
+ * sequence s is residues[offsets[s] .. offsets[s+1]).
+ */
+#ifndef MSV_H_
+#define MSV_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum msv_status {
+    MSV_OK = 0,
+    MSV_ERR_INVALID_ARGUMENT = 1, /* null pointer, bad size, bad offsets                       */
+    MSV_ERR_IO = 2,               /* file cannot be opened (reference: "Failed to open", Profile_HMM.cpp:50-53) */
+    MSV_ERR_PARSE = 3,            /* malformed .hmm / FASTA                                    */
+    MSV_ERR_BAD_RESIDUE = 4,      /* residue code >= 20 (reference: std::out_of_range from amino_acid_num.at, MSV_HMM.cpp:101) */
+    MSV_ERR_SEQUENCE_TOO_LONG = 5,/* longer than the device transition table (msv_profile_reserve_length) */
+    MSV_ERR_UNSUPPORTED_MODEL = 6,/* model length outside the compiled kernel family          */
+    MSV_ERR_NO_DEVICE = 7,        /* no HIP device / bad device ordinal                        */
+    MSV_ERR_HIP = 8,              /* a HIP runtime call failed                                 */
+    MSV_ERR_OUT_OF_MEMORY = 9
+} msv_status;
+
+typedef struct msv_hmm msv_hmm;         /* parsed HMMER3 profile (host)            */
+typedef struct msv_fasta msv_fasta;     /* parsed FASTA, residues packed as codes  */
+typedef struct msv_profile msv_profile; /* device-resident MSV scoring profile     */
+
+/* ---------------------------------------------------------------------------------------- */
+/* General                                                                                   */
+/* ---------------------------------------------------------------------------------------- */
+const char* msv_status_string(msv_status status);
+const char* msv_version(void);
+msv_status msv_device_count(int* count);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Host: HMMER3 profile parser -- replaces Profile_HMM::Profile_HMM (Profile_HMM.cpp:48-60)  */
+/* ---------------------------------------------------------------------------------------- */
+msv_status msv_hmm_read(const char* path, msv_hmm** out);
+void msv_hmm_destroy(msv_hmm* hmm);
+/* LENG + 1: includes the dummy node M0 (Profile_HMM.cpp:66-71) */
+size_t msv_hmm_model_length(const msv_hmm* hmm);
+const char* msv_hmm_name(const msv_hmm* hmm);
+/* {msv_mu, msv_lambda, viterbi_mu, viterbi_lambda, forward_theta, forward_lambda} (Profile_HMM.hpp:33-43) */
+void msv_hmm_stats(const msv_hmm* hmm, float out6[6]);
+/* probabilities exp(-x) as parsed (Profile_HMM.cpp:35-45): [model_length][20], [model_length][20], [model_length][7] */
+const float* msv_hmm_match_emissions(const msv_hmm* hmm);
+const float* msv_hmm_insert_emissions(const msv_hmm* hmm);
+const float* msv_hmm_transitions(const msv_hmm* hmm);
+
+/* MSV host precompute -- replaces MSV_HMM::MSV_HMM (MSV_HMM.cpp:35-57).
+ * emission_scores: caller buffer of 20 * model_length floats, residue-major,
+ * emission_scores[r * model_length + k] = logf(p_k[r] / bg[r]); column 0 = -inf. */
+msv_status msv_hmm_msv_scores(const msv_hmm* hmm, float* emission_scores, float* tr_B_Mk, float* tr_E_C,
+                              float* tr_E_J);
+
+/* Per-sequence transitions -- replaces MSV_HMM::init_transitions_depend_on_seq (MSV_HMM.cpp:59-64);
+ * L excludes the '#' sentinel. */
+void msv_sequence_transitions(uint64_t L, float* tr_loop, float* tr_move);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Host: FASTA reader -- replaces FASTA_protein_sequences (FASTA_protein_sequences.cpp:9-44) */
+/* Same record semantics (lines joined, records with a symbol outside the 20 amino acids     */
+/* dropped, empty records kept); residues are packed straight into the CSR code stream.     */
+/* A '#' inside a record is kept by the reference parser and only fails at scoring time;    */
+/* here it is stored as code 255, which the scorer rejects with MSV_ERR_BAD_RESIDUE.         */
+/* ---------------------------------------------------------------------------------------- */
+msv_status msv_fasta_read(const char* path, msv_fasta** out);
+void msv_fasta_destroy(msv_fasta* fasta);
+size_t msv_fasta_count(const msv_fasta* fasta);
+size_t msv_fasta_rejected(const msv_fasta* fasta);
+const uint8_t* msv_fasta_codes(const msv_fasta* fasta);     /* offsets[count] bytes   */
+const uint64_t* msv_fasta_offsets(const msv_fasta* fasta);  /* count + 1 entries      */
+const char* msv_fasta_header(const msv_fasta* fasta, size_t i); /* header line without '>' */
+
+/* Letters -> codes (A..Y -> 0..19).  Any other byte -> MSV_ERR_BAD_RESIDUE. */
+msv_status msv_encode_residues(const char* letters, size_t n, uint8_t* codes_out);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Device: the hot path -- replaces MSV_HMM::parallel_run_on_sequence (MSV_HMM.cpp:269-430) */
+/* and its 6 OpenCL kernels (MSV_kernels.cl:1-65, MSV_spec_kernels.cl:1-50) with ONE fused   */
+/* HIP kernel launch per batch.                                                              */
+/* ---------------------------------------------------------------------------------------- */
+
+/* Builds a device-resident profile from the precomputed MSV table (exactly what
+ * msv_hmm_msv_scores returns).  model_length = LENG + 1. */
+msv_status msv_profile_create(int device, const float* emission_scores, uint32_t model_length, float tr_B_Mk,
+                              float tr_E_C, float tr_E_J, msv_profile** out);
+/* Convenience: parse-side object straight to a device profile (MSV_HMM(const Profile_HMM&), MSV_HMM.hpp:19). */
+msv_status msv_profile_create_from_hmm(int device, const msv_hmm* hmm, msv_profile** out);
+void msv_profile_destroy(msv_profile* profile);
+
+typedef struct msv_kernel_info {
+    uint32_t model_length;     /* LENG + 1                                           */
+    uint32_t lanes_per_group;  /* G: lanes that own one sequence's DP row            */
+    uint32_t states_per_lane;  /* S: match states held in registers by each lane     */
+    uint32_t waves_per_block;  /* 64-lane waves per workgroup                        */
+    uint32_t lds_rows;         /* residue rows of the emission table staged in LDS   */
+    uint32_t lds_bytes;        /* LDS used per workgroup                             */
+    uint32_t blocks;           /* workgroups per launch (persistent grid)            */
+    uint32_t max_length;       /* longest sequence the transition table covers        */
+    int device;
+    char variant[64];
+} msv_kernel_info;
+msv_status msv_profile_describe(const msv_profile* profile, msv_kernel_info* out);
+
+/* Grow the per-sequence transition table so sequences up to max_length residues can be
+ * scored (default 131072). Host logf values, so the device never evaluates logf. */
+msv_status msv_profile_reserve_length(msv_profile* profile, uint64_t max_length);
+
+/* Host buffers in, host scores out; synchronous.  n = number of sequences; offsets has n+1
+ * entries, offsets[0] may be non-zero.  scores[s] = MSV log-odds score of sequence s, exactly
+ * MSV_HMM::run_on_sequence (MSV_HMM.cpp:74-113); an empty sequence scores -inf.
+ * stream may be NULL (the library's own stream). */
+msv_status msv_score_batch(msv_profile* profile, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
+                           float* scores, void* stream);
+
+/* Device-resident inputs and output (e.g. hipMalloc'd or torch tensors' data pointers), enqueued
+ * on `stream` (a hipStream_t, NULL = the library's stream) without a host synchronisation.
+ * residues_len = bytes addressable at d_residues (must be < 2^32 per call; split larger batches).
+ * d_order: optional permutation (n uint32) giving the order sequences are dequeued in
+ * (e.g. longest first); NULL = input order.  Errors found by the kernel (bad residue code,
+ * sequence longer than the table) are latched and returned by msv_profile_check. */
+msv_status msv_score_batch_device(msv_profile* profile, const uint8_t* d_residues, uint64_t residues_len,
+                                  const uint64_t* d_offsets, uint64_t n, const uint32_t* d_order, float* d_scores,
+                                  void* stream);
+
+/* Synchronises `stream` and returns (then clears) the errors latched by earlier device calls. */
+msv_status msv_profile_check(msv_profile* profile, void* stream);
+
+/* Device helper: writes a longest-first dequeue order for a device CSR batch into d_order
+ * (n uint32) using a counting sort on the device.  Enqueued on `stream`. */
+msv_status msv_order_longest_first(msv_profile* profile, const uint64_t* d_offsets, uint64_t n, uint32_t* d_order,
+                                   void* stream);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* MSV_H_ */

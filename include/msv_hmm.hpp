@@ -1,0 +1,110 @@
+// msv_hmm.hpp -- C++ host surface of the MI355X MSV engine, mirroring the reference classes
+// (drop-in names, argument meaning and layouts) on top of the C-ABI in msv.h:
+//
+//   Profile_HMM               data_readers/Profile_HMM.hpp:21-49
+//   FASTA_protein_sequences   data_readers/FASTA_protein_sequences.hpp:9-14
+//   MSV_HMM                   algorithms/MSV_HMM.hpp:17-44
+//
+// Differences from the reference, all deliberate:
+//   * errors throw (msv_error, or std::out_of_range for a residue outside the 20 amino acids,
+//     exactly what the reference's amino_acid_num.at throws, MSV_HMM.cpp:101) instead of printing
+//     and continuing with a half-built object (Profile_HMM.cpp:50-53, MSV_HMM.cpp:198-203);
+//   * run_on_sequence and parallel_run_on_sequence both score on the GPU (bit-identical to the
+//     reference CPU DP); the reference's sequential CPU DP lives only in oracle/ as the checker;
+//   * score_batch adds the batch API the reference lacks: one kernel launch per batch.
+#pragma once
+
+#include <array>
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "msv.h"
+
+constexpr int NUM_OF_AMINO_ACIDS = 20;
+constexpr int NUM_OF_TRANSITIONS = 7;
+
+using Probability = float;
+using Profile_name = std::string;
+template <int N>
+using Probabilities_array = std::array<Probability, N>;
+template <int N>
+using Probabilities_arrays_vector = std::vector<Probabilities_array<N>>;
+
+using Protein_sequence = std::string;  // '#' sentinel + residues, as the reference
+using Protein_sequences = std::vector<Protein_sequence>;
+using Log_score = float;
+
+class msv_error : public std::runtime_error {
+  public:
+    msv_error(msv_status s, const std::string& what) : std::runtime_error(what), status(s) {}
+    msv_status status;
+};
+
+class Profile_HMM {
+  public:
+    explicit Profile_HMM(const std::string& file_path);
+
+    Profile_name name;
+    Probabilities_arrays_vector<NUM_OF_AMINO_ACIDS> match_emissions;
+    Probabilities_arrays_vector<NUM_OF_AMINO_ACIDS> insert_emissions;
+    Probabilities_arrays_vector<NUM_OF_TRANSITIONS> transitions;
+    size_t model_length = 0;
+
+    float stats_local_msv_mu = 0, stats_local_msv_lambda = 0;
+    float stats_local_viterbi_mu = 0, stats_local_viterbi_lambda = 0;
+    float stats_local_forward_theta = 0, stats_local_forward_lambda = 0;
+};
+
+// Residues packed for the device: codes 0..19 (255 = a symbol the scorer rejects), CSR offsets.
+struct Packed_sequences {
+    std::vector<uint8_t> codes;
+    std::vector<uint64_t> offsets{0};
+    size_t size() const { return offsets.size() - 1; }
+    // '#'-prefixed strings -> codes; throws std::out_of_range on a symbol outside the 20
+    static Packed_sequences pack(const Protein_sequences& seqs);
+};
+
+class FASTA_protein_sequences {
+  public:
+    explicit FASTA_protein_sequences(const std::string& file_path);
+
+    Protein_sequences sequences;  // same records as the reference parser, '#'-prefixed
+    Packed_sequences packed;      // the same records as device-ready codes
+    std::vector<std::string> headers;
+    size_t rejected = 0;
+};
+
+class MSV_HMM {
+  public:
+    explicit MSV_HMM(const Profile_HMM& base_hmm, int device = 0);
+    ~MSV_HMM();
+    MSV_HMM(const MSV_HMM&) = delete;
+    MSV_HMM& operator=(const MSV_HMM&) = delete;
+    MSV_HMM(MSV_HMM&& o) noexcept;
+    MSV_HMM& operator=(MSV_HMM&& o) noexcept;
+
+    // One sequence ('#' + residues).  Scored by the same fused kernel as a batch of one.
+    Log_score run_on_sequence(const Protein_sequence& seq);
+    Log_score parallel_run_on_sequence(const Protein_sequence& seq, bool should_specialize = false);
+
+    // The batch hot path: one launch for the whole set.
+    std::vector<Log_score> score_batch(const Protein_sequences& seqs);
+    std::vector<Log_score> score_batch(const Packed_sequences& packed);
+    std::vector<Log_score> score_batch(const uint8_t* codes, const uint64_t* offsets, size_t n);
+
+    msv_profile* handle() { return profile_; }
+    size_t model_length() const { return model_length_; }
+    const std::vector<float>& emission_scores() const { return emission_scores_; }
+    float tr_B_Mk() const { return tr_B_Mk_; }
+    float tr_E_C() const { return tr_E_C_; }
+    float tr_E_J() const { return tr_E_J_; }
+
+  private:
+    size_t model_length_ = 0;
+    std::vector<float> emission_scores_;  // [20][model_length], MSV_HMM.hpp:27-28
+    float tr_B_Mk_ = 0, tr_E_C_ = 0, tr_E_J_ = 0;
+    msv_profile* profile_ = nullptr;
+};

@@ -1,0 +1,75 @@
+// test_msv.cpp -- GPU parity driver in the shape of the reference's differential test
+// (algorithms/test_MSV.cpp:14-36): every profile x fasta_like_example.fsa, scored through
+// run_on_sequence, parallel_run_on_sequence(seq) and parallel_run_on_sequence(seq, true),
+// plus the batch API.  Unlike the reference (which only checks seq vs par within 1e-4,
+// test_MSV.cpp:10-12,26), every score is compared BITWISE with the golden scores the
+// reference's own CPU path produced (tests/golden/example_scores.tsv, oracle/make_golden.py).
+// Usage: test_msv <repo_root>   (exit 0 = pass)
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "msv_hmm.hpp"
+
+static bool same_bits(float a, float b) { return std::memcmp(&a, &b, sizeof(float)) == 0; }
+
+int main(int argc, char** argv) {
+    const std::string root = argc > 1 ? argv[1] : ".";
+    std::map<std::string, std::vector<float>> golden;
+    std::ifstream g(root + "/tests/golden/example_scores.tsv");
+    std::string line;
+    while (std::getline(g, line)) {
+        if (line.empty() || line[0] == '#') continue;
+        std::istringstream ss(line);
+        std::string prof, idx, len, hex;
+        ss >> prof >> idx >> len >> hex;
+        golden[prof].push_back(std::strtof(hex.c_str(), nullptr));
+    }
+    if (golden.size() != 24) {
+        std::printf("test_msv: expected 24 profiles in golden file, got %zu\n", golden.size());
+        return 1;
+    }
+    auto fasta = FASTA_protein_sequences(root + "/data/FASTA_files/fasta_like_example.fsa");
+    int checked = 0;
+    for (const auto& [prof, want] : golden) {
+        auto msv = MSV_HMM(Profile_HMM(root + "/data/profile_HMMs/" + prof));
+        auto batch = msv.score_batch(fasta.sequences);
+        for (size_t i = 0; i < fasta.sequences.size(); ++i) {
+            const auto& protein = fasta.sequences[i];
+            float seq = msv.run_on_sequence(protein);
+            float par = msv.parallel_run_on_sequence(protein);
+            float par_spec = msv.parallel_run_on_sequence(protein, true);
+            if (!same_bits(seq, want[i]) || !same_bits(par, want[i]) || !same_bits(par_spec, want[i]) ||
+                !same_bits(batch[i], want[i])) {
+                std::printf("test_msv failed! %s seq %zu: golden %a, run %a, par %a, par_spec %a, batch %a\n",
+                            prof.c_str(), i, want[i], seq, par, par_spec, batch[i]);
+                return 1;
+            }
+            ++checked;
+        }
+    }
+    // error behaviour: a residue outside the 20 throws std::out_of_range like amino_acid_num.at
+    auto msv = MSV_HMM(Profile_HMM(root + "/data/profile_HMMs/100.hmm"));
+    bool threw = false;
+    try {
+        msv.run_on_sequence("#ACDXEF");
+    } catch (const std::out_of_range&) {
+        threw = true;
+    }
+    if (!threw) {
+        std::printf("test_msv failed! bad residue did not throw\n");
+        return 1;
+    }
+    if (!std::isinf(msv.run_on_sequence("#")) || msv.run_on_sequence("#") > 0) {
+        std::printf("test_msv failed! empty sequence must score -inf\n");
+        return 1;
+    }
+    std::printf("test_msv passed: %d scores bit-exact\n", checked);
+    return 0;
+}

@@ -1,0 +1,185 @@
+"""GPU parity: the fused gfx950 MSV kernel (through the C-ABI) against the golden scores of the
+reference's CPU path and the pinned oracle.  Tolerance: BITWISE (the north_star allows 1e-4; the
+kernel uses only IEEE add/max in the reference's order, so equality is expected and required).
+Size-independent properties cover BASELINE.json's full sizes."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import hmm_fasta_viterbi_amd as msv
+from hmm_fasta_viterbi_amd.synthetic import random_batch
+from oracle_lib import GOLD, PROFILES, ROOT, OracleProfile, bits, profile_path, read_golden_tsv
+
+_engines = {}
+
+
+def engine(prof: str) -> msv.MSV_HMM:
+    if prof not in _engines:
+        _engines[prof] = msv.MSV_HMM(msv.Profile_HMM(profile_path(prof)))
+    return _engines[prof]
+
+
+def test_device_visible():
+    assert msv.device_count() >= 1
+
+
+@pytest.mark.parametrize("prof", PROFILES)
+def test_example_fasta_every_profile(prof):
+    """test_MSV.cpp:14-36 inputs: every profile x fasta_like_example.fsa, via run_on_sequence,
+    parallel_run_on_sequence(seq), parallel_run_on_sequence(seq, True) and the batch API."""
+    fa = msv.FASTA_protein_sequences(os.path.join(ROOT, "data", "FASTA_files", "fasta_like_example.fsa"))
+    want = np.array([w for p, i, L, w in read_golden_tsv("example_scores.tsv") if p == prof], np.float32)
+    e = engine(prof)
+    got_batch = e.score_batch(fa.sequences)
+    assert np.array_equal(bits(got_batch), bits(want))
+    for i, s in enumerate(fa.sequences):
+        for got in (e.run_on_sequence(s), e.parallel_run_on_sequence(s), e.parallel_run_on_sequence(s, True)):
+            assert bits(got) == bits(want[i]), (prof, i, got, want[i])
+
+
+def test_random_fasta_3500():
+    fa = msv.FASTA_protein_sequences(os.path.join(ROOT, "data", "FASTA_files", "random_FASTA.fsa"))
+    rows = read_golden_tsv("random_fasta_scores.tsv")
+    for prof in PROFILES:
+        want = np.array([w for p, i, L, w in rows if p == prof], np.float32)
+        assert np.array_equal(bits(engine(prof).score_batch(fa.sequences)), bits(want)), prof
+
+
+@pytest.mark.parametrize("prof", ["100", "1400", "2405"])
+def test_seeded_golden_edge_lengths(prof):
+    """Lengths 0,1,2,3,...,257,1000,3500 + random, golden from the reference build."""
+    z = np.load(os.path.join(GOLD, f"seeded_{prof}.npz"))
+    got = engine(prof + ".hmm").score_batch(codes=z["codes"], offsets=z["offsets"])
+    assert np.array_equal(bits(got), bits(z["scores"]))
+
+
+def test_seeded_golden_every_profile():
+    z = np.load(os.path.join(GOLD, "seeded_all_profiles.npz"))
+    for prof in PROFILES:
+        k = prof.split(".")[0]
+        got = engine(prof).score_batch(codes=z[f"codes_{k}"], offsets=z[f"offsets_{k}"])
+        assert np.array_equal(bits(got), bits(z[f"scores_{k}"])), prof
+
+
+@pytest.mark.parametrize("prof,n,lmin,lmax,seed", [
+    ("100", 3000, 300, 500, 1),      # cfg2 shape (sample)
+    ("1400", 400, 300, 500, 2),      # cfg3 shape (sample)
+    ("2405", 60, 1500, 2500, 4),     # cfg5 shape (sample)
+    ("700", 500, 1, 900, 11),
+    ("1901", 200, 1, 1200, 12),
+    ("2050", 150, 1, 1500, 13),
+])
+def test_against_oracle_seeded(prof, n, lmin, lmax, seed):
+    codes, offsets = random_batch(seed, n, lmin, lmax)
+    want = OracleProfile(prof).score_batch(codes, offsets)
+    got = engine(prof + ".hmm").score_batch(codes=codes, offsets=offsets)
+    assert np.array_equal(bits(got), bits(want))
+
+
+def test_empty_and_degenerate_batches():
+    e = engine("1400.hmm")
+    # all empty -> -inf, no residue bytes at all
+    got = e.score_batch(codes=np.zeros(0, np.uint8), offsets=np.zeros(6, np.uint64))
+    assert np.all(np.isneginf(got))
+    # empty batch
+    assert e.score_batch(codes=np.zeros(0, np.uint8), offsets=np.zeros(1, np.uint64)).size == 0
+    # homopolymers and a single very long sequence mixed with empties
+    o = OracleProfile("1400")
+    for r in range(20):
+        codes = np.full(700, r, np.uint8)
+        offs = np.array([0, 0, 700, 700], np.uint64)
+        assert np.array_equal(bits(e.score_batch(codes=codes, offsets=offs)), bits(o.score_batch(codes, offs)))
+
+
+def test_bad_residue_raises_like_reference():
+    e = engine("100.hmm")
+    with pytest.raises(IndexError):
+        e.run_on_sequence("#ACDXEF")
+    with pytest.raises(IndexError):
+        e.score_batch(codes=np.array([0, 1, 20, 3], np.uint8), offsets=np.array([0, 4], np.uint64))
+    with pytest.raises(IndexError):  # '#' inside a record (kept by the FASTA reader)
+        e.run_on_sequence("#AC#DE")
+    # the profile stays usable after an error
+    assert np.isfinite(e.run_on_sequence("#ACDEF"))
+
+
+def test_long_sequence_grows_table():
+    e = engine("100.hmm")
+    codes, offsets = random_batch(77, 2, 140000, 150000)
+    want = OracleProfile("100").score_batch(codes, offsets)
+    assert np.array_equal(bits(e.score_batch(codes=codes, offsets=offsets)), bits(want))
+
+
+def test_device_api_with_torch_tensors_and_order():
+    torch = pytest.importorskip("torch")
+    e = engine("1400.hmm")
+    codes, offsets = random_batch(5, 3000, 1, 800)
+    dev = torch.device("cuda:0")
+    r = torch.from_numpy(codes).to(dev)
+    o = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    s = torch.empty(3000, dtype=torch.float32, device=dev)
+    order = torch.empty(3000, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    e.order_longest_first(o.data_ptr(), 3000, order.data_ptr(), stream)
+    e.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), 3000, s.data_ptr(), order.data_ptr(), stream)
+    e.check(stream)
+    got = s.cpu().numpy()
+    want = e.score_batch(codes=codes, offsets=offsets)
+    assert np.array_equal(bits(got), bits(want))
+    # the order is a permutation sorted by length, descending
+    perm = order.cpu().numpy().astype(np.int64)
+    assert np.array_equal(np.sort(perm), np.arange(3000))
+    lens = np.diff(offsets.astype(np.int64))[perm]
+    assert np.all(lens[:-1] >= lens[1:])
+    sample = np.arange(0, 3000, 37)
+    want_o = OracleProfile("1400").score_batch(*subset(codes, offsets, sample))
+    assert np.array_equal(bits(got[sample]), bits(want_o))
+
+
+def subset(codes, offsets, idx):
+    parts = [codes[int(offsets[i]):int(offsets[i + 1])] for i in idx]
+    offs = np.zeros(len(idx) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(p) for p in parts])
+    return (np.concatenate(parts) if parts else np.zeros(0, np.uint8)), offs
+
+
+def test_full_size_cfg3_properties():
+    """BASELINE cfg3 at full size (1400.hmm x 100k, len U[300,500]): determinism, permutation
+    invariance, and a seeded sample against the oracle."""
+    e = engine("1400.hmm")
+    codes, offsets = random_batch(2, 100_000, 300, 500)
+    a = e.score_batch(codes=codes, offsets=offsets)
+    b = e.score_batch(codes=codes, offsets=offsets)
+    assert np.array_equal(bits(a), bits(b))
+    assert np.all(np.isfinite(a))
+    perm = np.random.default_rng(0).permutation(100_000)[:5000]
+    pc, po = subset(codes, offsets, perm)
+    assert np.array_equal(bits(e.score_batch(codes=pc, offsets=po)), bits(a[perm]))
+    sample = perm[:60]
+    assert np.array_equal(bits(a[sample]), bits(OracleProfile("1400").score_batch(*subset(codes, offsets, sample))))
+
+
+def test_full_size_cfg5_sample():
+    """BASELINE cfg5 shape (2405.hmm, len U[1500,2500]) at 20k sequences + oracle sample."""
+    e = engine("2405.hmm")
+    codes, offsets = random_batch(4, 20_000, 1500, 2500)
+    a = e.score_batch(codes=codes, offsets=offsets)
+    sample = np.arange(0, 20_000, 1000)
+    assert np.array_equal(bits(a[sample]), bits(OracleProfile("2405").score_batch(*subset(codes, offsets, sample))))
+
+
+def test_cpp_parity_driver():
+    """tests/cpp/test_msv.cpp: the C++ MSV_HMM surface, every profile, bitwise vs golden."""
+    exe = os.path.join(ROOT, "hmm_fasta_viterbi_amd", "lib", "test_msv")
+    r = subprocess.run([exe, ROOT], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_describe_variant_for_1400():
+    d = engine("1400.hmm").describe()
+    assert d["model_length"] == 1401
+    assert d["lanes_per_group"] * d["states_per_lane"] >= 1400
