@@ -162,7 +162,10 @@ def main():
     d_off = torch.from_numpy(offsets.view(np.int64)).to(dev)
     d_scores = torch.empty(n, dtype=torch.float32, device=dev)
     d_order = torch.empty(n, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # A dedicated stream: torch's default (null) stream has handle 0, which the C-ABI reads as
+    # "use the library's own stream"; events must be recorded on the stream the kernel runs on.
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
     sh = stream.cuda_stream
     engine.reserve_length(lmax)
 

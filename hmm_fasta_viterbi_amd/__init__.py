@@ -184,6 +184,14 @@ class MSV_HMM:
     def reserve_length(self, max_length: int) -> None:
         check(_native.lib().msv_profile_reserve_length(self._p, max_length))
 
+    def set_variant(self, name: str) -> None:
+        check(_native.lib().msv_profile_set_variant(self._p, name.encode()), f"set_variant({name})")
+
+    @staticmethod
+    def variants() -> list[str]:
+        L = _native.lib()
+        return [L.msv_variant_name(i).decode() for i in range(L.msv_variant_count())]
+
     def describe(self) -> dict:
         info = _native.KernelInfo()
         check(_native.lib().msv_profile_describe(self._p, C.byref(info)))

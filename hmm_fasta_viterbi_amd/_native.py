@@ -36,7 +36,7 @@ EXPORTED = [
     "msv_fasta_offsets", "msv_fasta_header", "msv_encode_residues",
     "msv_profile_create", "msv_profile_create_from_hmm", "msv_profile_destroy", "msv_profile_describe",
     "msv_profile_reserve_length", "msv_score_batch", "msv_score_batch_device", "msv_profile_check",
-    "msv_order_longest_first",
+    "msv_order_longest_first", "msv_variant_count", "msv_variant_name", "msv_profile_set_variant",
 ]
 
 
@@ -78,6 +78,13 @@ def lib() -> C.CDLL:
         raise RuntimeError(
             f"{LIB_PATH} is missing: the MSV HIP library is not built. "
             "Run `python -c 'import __graft_entry__ as g; g.build()'` or `make -C hmm_fasta_viterbi_amd/csrc`.")
+    # One HIP runtime per process: torch ships its own libamdhip64 (soname libamdhip64.so.7, the
+    # same soname /opt/rocm's has).  Loading torch first makes our DT_NEEDED bind to torch's copy,
+    # so streams, events and device pointers from torch are valid handles for this library.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, sz, u64, u32, f32 = C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint32, C.c_float
     fp = C.POINTER(C.c_float)
@@ -112,6 +119,9 @@ def lib() -> C.CDLL:
         "msv_score_batch_device": (C.c_int, [vp, vp, u64, vp, u64, vp, vp, vp]),
         "msv_profile_check": (C.c_int, [vp, vp]),
         "msv_order_longest_first": (C.c_int, [vp, vp, u64, vp, vp]),
+        "msv_variant_count": (C.c_int, []),
+        "msv_variant_name": (C.c_char_p, [C.c_int]),
+        "msv_profile_set_variant": (C.c_int, [vp, C.c_char_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -81,7 +81,9 @@ msv_status hip_status(hipError_t e) {
 
 // Estimated issue cost of one row for one sequence: 2.5 VALU per state-slot plus the per-row
 // specials/reduction, times the lanes a sequence occupies.
-double variant_cost(const msvk::Variant& v) { return (2.5 * v.S + 26.0) * v.G * (v.big ? 1.6 : 1.0); }
+double variant_cost(const msvk::Variant& v) {
+    return (2.5 * v.S + 26.0) * v.G * (v.big ? 1.6 : 1.0) * (v.pf == 2 ? 1.0 : 1.05);
+}
 
 const msvk::Variant* pick_variant(uint32_t states) {
     int count = 0;
@@ -102,6 +104,7 @@ struct msv_profile {
     uint32_t model_length = 0;  // LENG + 1
     const msvk::Variant* v = nullptr;
     float tr_B_Mk = 0, tr_E_C = 0, tr_E_J = 0;
+    std::vector<float> emission_scores;  // host copy [20][model_length] (for re-layout)
     float4* d_etab = nullptr;
     float2* d_lentab = nullptr;
     uint32_t lentab_n = 0;
@@ -118,7 +121,52 @@ struct msv_profile {
     size_t d_off_cap = 0;
     float* d_scores = nullptr;
     size_t d_scores_cap = 0;
+    uint64_t* d_stamps = nullptr;  // diagnostic timeline buffer (tools only), or nullptr
+    uint32_t prio_shift = 5;       // wave-priority rotation period 2^k rows (0 = off)
 };
+
+
+// Lays the MSV table out for variant v and uploads it:
+// [row r][chunk c][lane gl] float4 = e[r][gl*S + 4c + 1 .. +4]; states beyond LENG are -inf
+// (never win a max); row 20 is the +inf poison row for codes >= 20.
+static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
+    const uint32_t model_length = p->model_length, R = model_length - 1;
+    const int G = v->G, S = v->S, C4 = S / 4;
+    std::vector<float> tab(static_cast<size_t>(msvk::kTableRows) * C4 * G * 4);
+    const float ninf = -std::numeric_limits<float>::infinity();
+    const float pinf = std::numeric_limits<float>::infinity();
+    for (int r = 0; r < msvk::kTableRows; ++r)
+        for (int c = 0; c < C4; ++c)
+            for (int gl = 0; gl < G; ++gl)
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t j = static_cast<uint32_t>(gl * S + 4 * c + q + 1);  // match state 1..
+                    float val;
+                    if (r == msvk::kPoisonRow) val = pinf;
+                    else val = (j <= R) ? p->emission_scores[static_cast<size_t>(r) * model_length + j] : ninf;
+                    tab[((static_cast<size_t>(r) * C4 + c) * G + gl) * 4 + q] = val;
+                }
+    float4* d = nullptr;
+    MSV_HIP(hipMalloc(reinterpret_cast<void**>(&d), tab.size() * sizeof(float)));
+    hipError_t e = hipMemcpy(d, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return hip_status(e);
+    }
+    if (p->d_etab) {
+        (void)hipStreamSynchronize(p->stream);
+        (void)hipFree(p->d_etab);
+    }
+    p->d_etab = d;
+    p->v = v;
+    hipDeviceProp_t prop;
+    MSV_HIP(hipGetDeviceProperties(&prop, p->device));
+    int per_cu = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(v->fn), v->waves * 64, 0);
+    if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    p->blocks = prop.multiProcessorCount * per_cu;
+    p->groups_per_block = v->waves * (64 / G);
+    return MSV_OK;
+}
 
 extern "C" {
 
@@ -240,46 +288,25 @@ msv_status msv_profile_create(int device, const float* emission_scores, uint32_t
     p->tr_E_C = tr_E_C;
     p->tr_E_J = tr_E_J;
 
-    // Kernel layout: [row r][chunk c][lane gl] float4 = e[r][gl*S + 4c + 1 .. +4]; states beyond
-    // LENG are -inf (never win a max); row 20 is the +inf poison row for codes >= 20.
-    const int G = v->G, S = v->S, C4 = S / 4;
-    std::vector<float> tab(static_cast<size_t>(msvk::kTableRows) * C4 * G * 4);
-    const float ninf = -std::numeric_limits<float>::infinity();
-    const float pinf = std::numeric_limits<float>::infinity();
-    for (int r = 0; r < msvk::kTableRows; ++r)
-        for (int c = 0; c < C4; ++c)
-            for (int gl = 0; gl < G; ++gl)
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t j = static_cast<uint32_t>(gl * S + 4 * c + q + 1);  // match state 1..
-                    float val;
-                    if (r == msvk::kPoisonRow) val = pinf;
-                    else val = (j <= R) ? emission_scores[static_cast<size_t>(r) * model_length + j] : ninf;
-                    tab[((static_cast<size_t>(r) * C4 + c) * G + gl) * 4 + q] = val;
-                }
-
-    auto fail = [&](hipError_t e) {
+    p->emission_scores.assign(emission_scores, emission_scores + static_cast<size_t>(20) * model_length);
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking)) != hipSuccess) {
         msv_profile_destroy(p);
         return hip_status(e);
-    };
-    hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_etab), tab.size() * sizeof(float))) != hipSuccess) return fail(e);
-    if ((e = hipMemcpy(p->d_etab, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
-        return fail(e);
-    if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_words), 4 * sizeof(uint32_t))) != hipSuccess) return fail(e);
-    if ((e = hipMemset(p->d_words, 0, 4 * sizeof(uint32_t))) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_dummy), 64)) != hipSuccess) return fail(e);
-    if ((e = hipMemset(p->d_dummy, 0, 64)) != hipSuccess) return fail(e);
-
-    hipDeviceProp_t prop;
-    if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return fail(e);
-    int per_cu = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(v->fn), v->waves * 64, 0);
-    if (e != hipSuccess || per_cu < 1) per_cu = 1;
-    p->blocks = prop.multiProcessorCount * per_cu;
-    p->groups_per_block = v->waves * (64 / G);
-
-    msv_status s = msv_profile_reserve_length(p, kDefaultMaxLength - 1);
+    }
+    if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_words), 4 * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMemset(p->d_words, 0, 4 * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void**>(&p->d_dummy), 64)) != hipSuccess ||
+        (e = hipMemset(p->d_dummy, 0, 64)) != hipSuccess) {
+        msv_profile_destroy(p);
+        return hip_status(e);
+    }
+    msv_status s = install_variant(p, v);
+    if (s != MSV_OK) {
+        msv_profile_destroy(p);
+        return s;
+    }
+    s = msv_profile_reserve_length(p, kDefaultMaxLength - 1);
     if (s != MSV_OK) {
         msv_profile_destroy(p);
         return s;
@@ -287,6 +314,49 @@ msv_status msv_profile_create(int device, const float* emission_scores, uint32_t
     *out = p;
     return MSV_OK;
 }
+
+int msv_variant_count(void) {
+    int count = 0;
+    (void)msvk::variants(&count);
+    return count;
+}
+
+const char* msv_variant_name(int i) {
+    int count = 0;
+    const msvk::Variant* all = msvk::variants(&count);
+    return (i >= 0 && i < count) ? all[i].name : nullptr;
+}
+
+msv_status msv_profile_set_variant(msv_profile* p, const char* name) {
+    if (!p || !name) return MSV_ERR_INVALID_ARGUMENT;
+    int count = 0;
+    const msvk::Variant* all = msvk::variants(&count);
+    for (int i = 0; i < count; ++i) {
+        if (std::strcmp(all[i].name, name) != 0) continue;
+        if (static_cast<uint32_t>(all[i].G * all[i].S) < p->model_length - 1) return MSV_ERR_UNSUPPORTED_MODEL;
+        DeviceGuard g(p->device);
+        if (!g.ok) return MSV_ERR_NO_DEVICE;
+        return install_variant(p, &all[i]);
+    }
+    return MSV_ERR_INVALID_ARGUMENT;
+}
+
+// Diagnostics, deliberately not in msv.h: a device buffer of 4 uint64 per wave of the persistent
+// grid that receives {start, end (s_memrealtime, 100 MHz), rows issued, xcc<<32|block} for every
+// wave of subsequent launches (tools/wave_timeline.py).  nullptr switches it off.
+msv_status msv_debug_set_stamps(msv_profile* p, uint64_t* d_stamps) {
+    if (!p) return MSV_ERR_INVALID_ARGUMENT;
+    p->d_stamps = d_stamps;
+    return MSV_OK;
+}
+
+msv_status msv_debug_set_prio_shift(msv_profile* p, uint32_t k) {
+    if (!p || k > 16) return MSV_ERR_INVALID_ARGUMENT;
+    p->prio_shift = k;
+    return MSV_OK;
+}
+
+int msv_debug_grid_waves(const msv_profile* p) { return p ? p->blocks * p->v->waves : 0; }
 
 msv_status msv_profile_create_from_hmm(int device, const msv_hmm* hmm, msv_profile** out) {
     if (!hmm || !out) return MSV_ERR_INVALID_ARGUMENT;
@@ -339,6 +409,8 @@ msv_status msv_score_batch_device(msv_profile* p, const uint8_t* d_residues, uin
     a.tr_B_Mk = p->tr_B_Mk;
     a.tr_E_C = p->tr_E_C;
     a.tr_E_J = p->tr_E_J;
+    a.stamps = p->d_stamps;
+    a.prio_shift = p->prio_shift;
 
     const uint64_t want = (n + p->groups_per_block - 1) / p->groups_per_block;
     const int blocks = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(p->blocks), want));

@@ -108,7 +108,7 @@ __device__ __forceinline__ uint32_t group_dequeue(uint32_t* counter, bool leader
 
 }  // namespace
 
-template <int G, int S, int WAVES, bool BIG>
+template <int G, int S, int WAVES, int PF, bool BIG>
 __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs a) {
     static_assert(S % 4 == 0, "S must be a multiple of 4 (float4 chunks)");
     constexpr int C4 = S / 4;
@@ -186,45 +186,72 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     begin();
     uint32_t r0 = res[pos];
     uint32_t r1 = res[min(pos + 1, endpos)];
+    uint64_t t_start = 0;
+    if (a.stamps) t_start = __builtin_amdgcn_s_memrealtime();
+    uint32_t rows_done = 0;
 
     while (__any(active)) {
         const uint32_t r2 = res[min(pos + 2, endpos)];
         const uint32_t rr = min(r0, static_cast<uint32_t>(kPoisonRow));
 
-        float4 e[C4];
+        const float4* ep;
         if constexpr (!BIG) {
-            const float4* ep = &tab[rr * ROW_F4 + gl];
-#pragma unroll
-            for (int c = 0; c < C4; ++c) e[c] = ep[c * G];
+            ep = &tab[rr * ROW_F4 + gl];
         } else {
-            const float4* ep = (rr < static_cast<uint32_t>(LDS_ROWS)) ? &tab[rr * ROW_F4 + gl]
-                                                                      : &a.etab[rr * ROW_F4 + gl];
-#pragma unroll
-            for (int c = 0; c < C4; ++c) e[c] = ep[c * G];
+            ep = (rr < static_cast<uint32_t>(LDS_ROWS)) ? &tab[rr * ROW_F4 + gl] : &a.etab[rr * ROW_F4 + gl];
         }
-
         const float Bt = B + trBMk;
         const float nbr = shift_in<G>(M[S - 1], NINF);
+        float Elane;
 
-        // Update in place from the highest state down, so M[k-1] is still the previous row.
+        if constexpr (PF == 0) {
+            // All S emissions in flight at once (S extra VGPRs), compiler-scheduled.
+            float4 e[C4];
 #pragma unroll
-        for (int k = S - 1; k >= 1; --k) {
-            const float4 ev = e[k >> 2];
-            const float ek = (k & 3) == 0 ? ev.x : (k & 3) == 1 ? ev.y : (k & 3) == 2 ? ev.z : ev.w;
-            M[k] = ek + fmaxf(M[k - 1], Bt);
-        }
-        M[0] = e[0].x + fmaxf(nbr, Bt);
-
-        // E = max_j M_j : four independent max3 chains, then the group butterfly.
-        float p0 = M[0], p1 = M[1], p2 = M[2], p3 = M[3];
+            for (int c = 0; c < C4; ++c) e[c] = ep[c * G];
+            // Update in place from the highest state down, so M[k-1] is still the previous row.
 #pragma unroll
-        for (int k = 4; k < S; k += 4) {
-            p0 = fmaxf(p0, M[k]);
-            p1 = fmaxf(p1, M[k + 1]);
-            p2 = fmaxf(p2, M[k + 2]);
-            p3 = fmaxf(p3, M[k + 3]);
+            for (int k = S - 1; k >= 1; --k) {
+                const float4 ev = e[k >> 2];
+                const float ek = (k & 3) == 0 ? ev.x : (k & 3) == 1 ? ev.y : (k & 3) == 2 ? ev.z : ev.w;
+                M[k] = ek + fmaxf(M[k - 1], Bt);
+            }
+            M[0] = e[0].x + fmaxf(nbr, Bt);
+            // E = max_j M_j : four independent max3 chains
+            float p0 = M[0], p1 = M[1], p2 = M[2], p3 = M[3];
+#pragma unroll
+            for (int k = 4; k < S; k += 4) {
+                p0 = fmaxf(p0, M[k]);
+                p1 = fmaxf(p1, M[k + 1]);
+                p2 = fmaxf(p2, M[k + 2]);
+                p3 = fmaxf(p3, M[k + 3]);
+            }
+            Elane = fmaxf(fmaxf(p0, p1), fmaxf(p2, p3));
+        } else {
+            // Streamed: a ring of PF float4 chunks in flight, one chunk (4 states) consumed per
+            // step, scheduling pinned per chunk so only PF*4 emission VGPRs are live -> fewer
+            // VGPRs, more waves per SIMD to hide the per-row serial section.
+            float4 ring[PF];
+#pragma unroll
+            for (int d = 0; d < PF; ++d) ring[d] = ep[(C4 - 1 - d) * G];
+            float p0 = NINF, p1 = NINF;
+#pragma unroll
+            for (int c = C4 - 1; c >= 0; --c) {
+                const int slot = (C4 - 1 - c) % PF;
+                const float4 ev = ring[slot];
+                if (c - PF >= 0) ring[slot] = ep[(c - PF) * G];
+                const int k = 4 * c;
+                M[k + 3] = ev.w + fmaxf(M[k + 2], Bt);
+                M[k + 2] = ev.z + fmaxf(M[k + 1], Bt);
+                M[k + 1] = ev.y + fmaxf(M[k], Bt);
+                M[k] = ev.x + fmaxf(c == 0 ? nbr : M[k - 1], Bt);
+                p0 = fmaxf(fmaxf(p0, M[k + 3]), M[k + 2]);
+                p1 = fmaxf(fmaxf(p1, M[k + 1]), M[k]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            Elane = fmaxf(p0, p1);
         }
-        const float E = group_max<G>(fmaxf(fmaxf(p0, p1), fmaxf(p2, p3)));
+        const float E = group_max<G>(Elane);
 
         J = fmaxf(J + loop, E + tEJ);
         C = fmaxf(C + loop, E + tEC);
@@ -245,6 +272,31 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             r0 = res[pos];
             r1 = res[min(pos + 1, endpos)];
         }
+        ++rows_done;
+        // Rotate issue priority among the waves sharing a SIMD (waves w, w+4, w+8, w+12 of the
+        // workgroup): VALU issue is arbitrated by priority, then age, so without this the oldest
+        // wave runs ~2.5x faster than the youngest and the slow waves' last sequences form a long
+        // tail after the queue drains.  Rotation equalises their progress.
+        if (a.prio_shift && (rows_done & ((1u << a.prio_shift) - 1)) == 0) {
+            switch (((rows_done >> a.prio_shift) + (threadIdx.x >> 8)) & 3) {
+                case 0: __builtin_amdgcn_s_setprio(0); break;
+                case 1: __builtin_amdgcn_s_setprio(1); break;
+                case 2: __builtin_amdgcn_s_setprio(2); break;
+                default: __builtin_amdgcn_s_setprio(3); break;
+            }
+        }
+    }
+    // Diagnostic only (a.stamps == nullptr in production): per-wave start/end realtime (100 MHz),
+    // rows issued, XCC id.  Never read by the kernel; used by tools/wave_timeline.py.
+    if (a.stamps && lane == 0) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        const uint32_t w = blockIdx.x * WAVES + (threadIdx.x >> 6);
+        uint32_t xcc = 0;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        a.stamps[4 * w + 0] = t_start;
+        a.stamps[4 * w + 1] = t_end;
+        a.stamps[4 * w + 2] = rows_done;
+        a.stamps[4 * w + 3] = (static_cast<uint64_t>(xcc) << 32) | blockIdx.x;
     }
 }
 
@@ -302,10 +354,11 @@ __global__ void order_scatter_kernel(const uint64_t* __restrict__ offsets, uint6
 // covers LENG with the least estimated cost (the analog of the reference's should_specialize,
 // which bakes sizes into the OpenCL program with -D defines, MSV_HMM.cpp:322-337).
 // ------------------------------------------------------------------------------------------------
-#define MSV_VARIANT(G_, S_, W_)                                                                             \
-    Variant{G_, S_, W_, lds_rows_for(G_, S_), lds_rows_for(G_, S_) < kTableRows,                            \
-            reinterpret_cast<const void*>(&msv_batch_kernel<G_, S_, W_, (lds_rows_for(G_, S_) < kTableRows)>), \
-            "msv_g" #G_ "_s" #S_ "_w" #W_}
+#define MSV_VARIANT(G_, S_, W_, P_)                                                                       \
+    Variant{G_, S_, W_, P_, lds_rows_for(G_, S_), lds_rows_for(G_, S_) < kTableRows,                      \
+            reinterpret_cast<const void*>(                                                                 \
+                &msv_batch_kernel<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows)>),                   \
+            "msv_g" #G_ "_s" #S_ "_w" #W_ "_p" #P_}
 
 static const Variant kVariants[] = {
 #include "msv_variants.inc"

@@ -121,6 +121,13 @@ typedef struct msv_kernel_info {
 } msv_kernel_info;
 msv_status msv_profile_describe(const msv_profile* profile, msv_kernel_info* out);
 
+/* The compiled kernel family (template instantiations over G, S, waves; names "msv_g<G>_s<S>_w<W>").
+ * msv_profile_create picks the cheapest variant with G*S >= LENG; msv_profile_set_variant forces
+ * another one (tuning / tests).  Every variant returns identical scores. */
+int msv_variant_count(void);
+const char* msv_variant_name(int i);
+msv_status msv_profile_set_variant(msv_profile* profile, const char* name);
+
 /* Grow the per-sequence transition table so sequences up to max_length residues can be
  * scored (default 131072). Host logf values, so the device never evaluates logf. */
 msv_status msv_profile_reserve_length(msv_profile* profile, uint64_t max_length);

@@ -1,0 +1,50 @@
+"""Run the MSV kernel alone on a BASELINE config (for rocprofv3 --kernel-trace / --pmc passes).
+
+    python tools/run_kernel.py --config cfg3 --launches 5 [--variant NAME] [--no-order]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg3")
+    ap.add_argument("--launches", type=int, default=5)
+    ap.add_argument("--variant", default="")
+    ap.add_argument("--no-order", action="store_true")
+    args = ap.parse_args()
+    import torch
+    import hmm_fasta_viterbi_amd as msv
+    from hmm_fasta_viterbi_amd.synthetic import random_batch
+    from bench import CONFIGS
+
+    prof, n, lmin, lmax, seed = CONFIGS[args.config]
+    eng = msv.MSV_HMM(msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof)))
+    if args.variant:
+        eng.set_variant(args.variant)
+    codes, offsets = random_batch(seed * 1000, n, lmin, lmax)
+    dev = torch.device("cuda:0")
+    st = torch.cuda.Stream(dev)
+    r = torch.from_numpy(codes).to(dev)
+    o = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    s = torch.empty(n, dtype=torch.float32, device=dev)
+    order = torch.empty(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    if not args.no_order:
+        eng.order_longest_first(o.data_ptr(), n, order.data_ptr(), st.cuda_stream)
+    op = None if args.no_order else order.data_ptr()
+    for _ in range(args.launches):
+        eng.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), n, s.data_ptr(), op, st.cuda_stream)
+    eng.check(st.cuda_stream)
+    print(f"{args.config}: {eng.describe()['variant']} x {args.launches} launches, residues={int(offsets[-1])}, "
+          f"LENG={eng.model_length - 1}")
+
+
+if __name__ == "__main__":
+    main()
