@@ -22,7 +22,7 @@
 namespace {
 
 constexpr uint32_t kDefaultMaxLength = 131072;
-constexpr uint32_t kOrderBins = 1u << 16;
+constexpr uint32_t kOrderBins = 4096;  // lengths >= 4095 share the longest bin
 
 struct DeviceGuard {
     int prev = -1;

@@ -37,6 +37,7 @@
 //     (host logf, so scores never depend on a device logf).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "msv_kernel.h"
@@ -301,50 +302,73 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
 }
 
 // ------------------------------------------------------------------------------------------------
-// Longest-first dequeue order (counting sort on the device): hist -> scan -> scatter.
+// Longest-first dequeue order: a device counting sort on sequence length (lengths >= nbins-1 share
+// the first bin).  Three small launches, histograms privatised in LDS so global atomics are one
+// per (block, non-empty bin):  count -> scan -> place.  Order inside a bin is arbitrary (it never
+// changes a score: every score is written to its own sequence's slot).
 // ------------------------------------------------------------------------------------------------
-__global__ void order_hist_kernel(const uint64_t* __restrict__ offsets, uint64_t n, uint32_t* __restrict__ hist,
-                                  uint32_t nbins) {
-    for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < n; s += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t L = offsets[s + 1] - offsets[s];
-        uint32_t b = L >= nbins ? nbins - 1 : static_cast<uint32_t>(L);
-        atomicAdd(&hist[nbins - 1 - b], 1u);  // descending length
+constexpr int kOrderThreads = 1024;
+
+__device__ __forceinline__ uint32_t length_bin(const uint64_t* __restrict__ offsets, uint64_t s, uint32_t nbins) {
+    const uint64_t L = offsets[s + 1] - offsets[s];
+    return nbins - 1 - static_cast<uint32_t>(L >= nbins - 1 ? nbins - 1 : L);  // descending length
+}
+
+__global__ __launch_bounds__(kOrderThreads) void order_count_kernel(const uint64_t* __restrict__ offsets, uint64_t n,
+                                                                    uint64_t chunk, uint32_t* __restrict__ hist,
+                                                                    uint32_t nbins) {
+    extern __shared__ uint32_t lh[];
+    for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x) lh[i] = 0;
+    __syncthreads();
+    const uint64_t lo = blockIdx.x * chunk, hi = min(n, lo + chunk);
+    for (uint64_t s = lo + threadIdx.x; s < hi; s += blockDim.x) atomicAdd(&lh[length_bin(offsets, s, nbins)], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x)
+        if (lh[i]) atomicAdd(&hist[i], lh[i]);
+}
+
+// Exclusive scan of hist[nbins] in place (one block; nbins <= 4 * kOrderThreads).
+__global__ __launch_bounds__(kOrderThreads) void order_scan_kernel(uint32_t* __restrict__ hist, uint32_t nbins) {
+    __shared__ uint32_t part[kOrderThreads];
+    const uint32_t t = threadIdx.x;
+    uint32_t v[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = 4 * t + q;
+        v[q] = i < nbins ? hist[i] : 0u;
+        sum += v[q];
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < kOrderThreads; d <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t x = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = 4 * t + q;
+        if (i < nbins) hist[i] = run;
+        run += v[q];
     }
 }
 
-__global__ void order_scan_kernel(uint32_t* __restrict__ hist, uint32_t nbins) {
-    // single block exclusive scan, in place (nbins is small: <= 1 << 16)
-    __shared__ uint32_t partial[1024];
-    const uint32_t t = threadIdx.x, T = blockDim.x;
-    const uint32_t per = (nbins + T - 1) / T;
-    const uint32_t lo = t * per, hi = min(nbins, lo + per);
-    uint32_t sum = 0;
-    for (uint32_t i = lo; i < hi; ++i) sum += hist[i];
-    partial[t] = sum;
+__global__ __launch_bounds__(kOrderThreads) void order_place_kernel(const uint64_t* __restrict__ offsets, uint64_t n,
+                                                                    uint64_t chunk, uint32_t* __restrict__ cursor,
+                                                                    uint32_t nbins, uint32_t* __restrict__ order) {
+    extern __shared__ uint32_t lh[];  // [0, nbins): block counts, then block cursors
+    for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x) lh[i] = 0;
     __syncthreads();
-    if (t == 0) {
-        uint32_t run = 0;
-        for (uint32_t i = 0; i < T; ++i) {
-            uint32_t v = partial[i];
-            partial[i] = run;
-            run += v;
-        }
-    }
+    const uint64_t lo = blockIdx.x * chunk, hi = min(n, lo + chunk);
+    for (uint64_t s = lo + threadIdx.x; s < hi; s += blockDim.x) atomicAdd(&lh[length_bin(offsets, s, nbins)], 1u);
     __syncthreads();
-    uint32_t run = partial[t];
-    for (uint32_t i = lo; i < hi; ++i) {
-        uint32_t v = hist[i];
-        hist[i] = run;
-        run += v;
-    }
-}
-
-__global__ void order_scatter_kernel(const uint64_t* __restrict__ offsets, uint64_t n, uint32_t* __restrict__ cursor,
-                                     uint32_t nbins, uint32_t* __restrict__ order) {
-    for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < n; s += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t L = offsets[s + 1] - offsets[s];
-        uint32_t b = L >= nbins ? nbins - 1 : static_cast<uint32_t>(L);
-        uint32_t slot = atomicAdd(&cursor[nbins - 1 - b], 1u);
+    for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x)
+        if (lh[i]) lh[i] = atomicAdd(&cursor[i], lh[i]);  // reserve this block's range of bin i
+    __syncthreads();
+    for (uint64_t s = lo + threadIdx.x; s < hi; s += blockDim.x) {
+        const uint32_t slot = atomicAdd(&lh[length_bin(offsets, s, nbins)], 1u);
         order[slot] = static_cast<uint32_t>(s);
     }
 }
@@ -376,12 +400,17 @@ hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, h
 
 hipError_t launch_order(const uint64_t* offsets, uint64_t n, uint32_t* scratch_hist, uint32_t nbins, uint32_t* order,
                         hipStream_t stream) {
+    if (nbins > 4 * kOrderThreads) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(scratch_hist, 0, nbins * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    const uint32_t blocks = static_cast<uint32_t>(n / 256 + 1 > 1024 ? 1024 : n / 256 + 1);
-    hipLaunchKernelGGL(order_hist_kernel, dim3(blocks), dim3(256), 0, stream, offsets, n, scratch_hist, nbins);
-    hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(1024), 0, stream, scratch_hist, nbins);
-    hipLaunchKernelGGL(order_scatter_kernel, dim3(blocks), dim3(256), 0, stream, offsets, n, scratch_hist, nbins, order);
+    const uint64_t blocks = std::min<uint64_t>(256, (n + 511) / 512);
+    const uint64_t chunk = (n + blocks - 1) / blocks;
+    const size_t lds = nbins * sizeof(uint32_t);
+    hipLaunchKernelGGL(order_count_kernel, dim3(blocks), dim3(kOrderThreads), lds, stream, offsets, n, chunk,
+                       scratch_hist, nbins);
+    hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(kOrderThreads), 0, stream, scratch_hist, nbins);
+    hipLaunchKernelGGL(order_place_kernel, dim3(blocks), dim3(kOrderThreads), lds, stream, offsets, n, chunk,
+                       scratch_hist, nbins, order);
     return hipGetLastError();
 }
 
