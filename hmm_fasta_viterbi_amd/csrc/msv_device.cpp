@@ -82,7 +82,7 @@ msv_status hip_status(hipError_t e) {
 // Estimated issue cost of one row for one sequence: 2.5 VALU per state-slot plus the per-row
 // specials/reduction, times the lanes a sequence occupies.
 double variant_cost(const msvk::Variant& v) {
-    return (2.5 * v.S + 26.0) * v.G * (v.big ? 1.6 : 1.0) * (v.pf == 2 ? 1.0 : 1.05);
+    return (2.5 * v.S + 26.0) * v.G * (v.big ? 1.6 : 1.0) * (v.pf == 2 ? 1.0 : 1.05) * (v.streams == 2 ? 1.15 : 1.0);
 }
 
 const msvk::Variant* pick_variant(uint32_t states) {
@@ -108,7 +108,7 @@ struct msv_profile {
     float4* d_etab = nullptr;
     float2* d_lentab = nullptr;
     uint32_t lentab_n = 0;
-    uint32_t* d_words = nullptr;  // [0] dequeue counter, [1] sticky error bits
+    uint32_t* d_words = nullptr;  // [0] dequeue counter, [2] sticky error bits
     uint32_t* d_hist = nullptr;   // longest-first counting-sort scratch
     uint8_t* d_dummy = nullptr;   // a readable residue byte for batches with no residues
     hipStream_t stream = nullptr;
@@ -122,7 +122,6 @@ struct msv_profile {
     float* d_scores = nullptr;
     size_t d_scores_cap = 0;
     uint64_t* d_stamps = nullptr;  // diagnostic timeline buffer (tools only), or nullptr
-    uint32_t prio_shift = 5;       // wave-priority rotation period 2^k rows (0 = off)
 };
 
 
@@ -164,7 +163,7 @@ static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(v->fn), v->waves * 64, 0);
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
     p->blocks = prop.multiProcessorCount * per_cu;
-    p->groups_per_block = v->waves * (64 / G);
+    p->groups_per_block = v->waves * (64 / G) * v->streams;
     return MSV_OK;
 }
 
@@ -350,12 +349,6 @@ msv_status msv_debug_set_stamps(msv_profile* p, uint64_t* d_stamps) {
     return MSV_OK;
 }
 
-msv_status msv_debug_set_prio_shift(msv_profile* p, uint32_t k) {
-    if (!p || k > 16) return MSV_ERR_INVALID_ARGUMENT;
-    p->prio_shift = k;
-    return MSV_OK;
-}
-
 int msv_debug_grid_waves(const msv_profile* p) { return p ? p->blocks * p->v->waves : 0; }
 
 msv_status msv_profile_create_from_hmm(int device, const msv_hmm* hmm, msv_profile** out) {
@@ -403,14 +396,13 @@ msv_status msv_score_batch_device(msv_profile* p, const uint8_t* d_residues, uin
     a.lentab = p->d_lentab;
     a.scores = d_scores;
     a.counter = p->d_words;
-    a.errors = p->d_words + 1;
+    a.errors = p->d_words + 2;
     a.n = n;
     a.lentab_n = p->lentab_n;
     a.tr_B_Mk = p->tr_B_Mk;
     a.tr_E_C = p->tr_E_C;
     a.tr_E_J = p->tr_E_J;
     a.stamps = p->d_stamps;
-    a.prio_shift = p->prio_shift;
 
     const uint64_t want = (n + p->groups_per_block - 1) / p->groups_per_block;
     const int blocks = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(p->blocks), want));
@@ -425,9 +417,9 @@ msv_status msv_profile_check(msv_profile* p, void* stream) {
     if (!g.ok) return MSV_ERR_NO_DEVICE;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p->stream;
     uint32_t err = 0;
-    MSV_HIP(hipMemcpyAsync(&err, p->d_words + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    MSV_HIP(hipMemcpyAsync(&err, p->d_words + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     MSV_HIP(hipStreamSynchronize(st));
-    if (err) MSV_HIP(hipMemsetAsync(p->d_words + 1, 0, sizeof(uint32_t), st));
+    if (err) MSV_HIP(hipMemsetAsync(p->d_words + 2, 0, sizeof(uint32_t), st));
     MSV_HIP(hipStreamSynchronize(st));
     if (err & msvk::kErrBadResidue) return MSV_ERR_BAD_RESIDUE;
     if (err & msvk::kErrTooLong) return MSV_ERR_SEQUENCE_TOO_LONG;

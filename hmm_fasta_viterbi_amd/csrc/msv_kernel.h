@@ -33,11 +33,10 @@ struct KernelArgs {
     uint32_t lentab_n;
     float tr_B_Mk, tr_E_C, tr_E_J;
     uint64_t* stamps;          // diagnostic per-wave timeline (nullptr in production)
-    uint32_t prio_shift;       // rotate wave priority every 2^prio_shift rows (0 = off)
 };
 
 struct Variant {
-    int G, S, waves, pf;  // pf = emission prefetch ring depth (0 = all chunks at once)
+    int G, S, waves, pf, streams;  // pf = emission ring depth; streams = sequences per lane group
     int lds_rows;
     bool big;
     const void* fn;

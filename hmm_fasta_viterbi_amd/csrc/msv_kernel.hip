@@ -39,6 +39,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <type_traits>
+#include <utility>
 
 #include "msv_kernel.h"
 
@@ -100,8 +102,9 @@ __device__ __forceinline__ uint32_t group_bcast(uint32_t v, int lane) {
     return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute((lane & ~(G - 1)) << 2, static_cast<int>(v)));
 }
 
+// Next sequence index for the whole group (one atomic by the group leader, broadcast).
 template <int G>
-__device__ __forceinline__ uint32_t group_dequeue(uint32_t* counter, bool leader, int lane) {
+__device__ __forceinline__ uint32_t group_take(uint32_t* counter, bool leader, int lane) {
     uint32_t v = 0;
     if (leader) v = atomicAdd(counter, 1u);
     return group_bcast<G>(v, lane);
@@ -109,9 +112,30 @@ __device__ __forceinline__ uint32_t group_dequeue(uint32_t* counter, bool leader
 
 }  // namespace
 
-template <int G, int S, int WAVES, int PF, bool BIG>
+// Per-lane state of one sequence being scored (one "stream"): S match states of the DP row in
+// VGPRs, the specials, and the residue cursor.  Separate objects (never an indexed array) so all of
+// it stays in registers.
+template <int S>
+struct Stream {
+    float M[S];
+    float J, C, N, B, loop, move;
+    uint32_t pos, endpos, rows_left, seq, len, r0;  // r0 = residue code of the next row (prefetched)
+    bool active;
+};
+
+// Per-row working set of one stream.
+template <int PF>
+struct RowCtx {
+    const float4* ep;
+    float Bt, nbr, p0, p1, p2, p3;
+    uint32_t r1;
+    float4 ring[PF];
+};
+
+template <int G, int S, int WAVES, int PF, bool BIG, int D, int EXP = 0>
 __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs a) {
     static_assert(S % 4 == 0, "S must be a multiple of 4 (float4 chunks)");
+    static_assert(PF >= 1 && D >= 1 && D <= 2, "PF >= 1, D in {1, 2}");
     constexpr int C4 = S / 4;
     constexpr int ROW_F4 = C4 * G;  // float4 per residue row
     constexpr int LDS_ROWS = lds_rows_for(G, S);
@@ -130,31 +154,41 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     const uint8_t* __restrict__ res = a.residues;
     const float trBMk = a.tr_B_Mk, tEC = a.tr_E_C, tEJ = a.tr_E_J;
 
-    float M[S];
-    float J = NINF, C = NINF, N = 0.f, B = 0.f, loop = 0.f, move = 0.f;
-    uint32_t pos = 0, endpos = 0, rows_left = 0xFFFFFFFFu, seq = 0;
-    bool active = false;
-#pragma unroll
-    for (int k = 0; k < S; ++k) M[k] = NINF;
+    uint32_t rows_done = 0;  // rows issued by this wave (diagnostics)
+    // Sequence indices are prefetched one ahead (the atomic's latency hides behind a sequence).
+    uint32_t cur = group_take<G>(a.counter, leader, lane);
+    uint32_t nxt = group_take<G>(a.counter, leader, lane);
 
-    uint32_t cur = group_dequeue<G>(a.counter, leader, lane);
-    uint32_t nxt = group_dequeue<G>(a.counter, leader, lane);
-
-    // Start the next non-empty sequence of this group (or retire the group).
-    auto begin = [&]() {
+    // Start the next non-empty sequence in a stream (or retire the stream).
+    auto begin = [&](Stream<S>& st) {
         for (;;) {
-            if (cur >= a.n) {
-                active = false;
-                pos = 0;
-                endpos = 0;
-                rows_left = 0xFFFFFFFFu;
+            const uint32_t idx = cur;
+            cur = nxt;
+            nxt = group_take<G>(a.counter, leader, lane);
+            if (idx >= a.n) {
+                // Retire: assign exactly the fields the start path assigns (otherwise the compiler
+                // merges the two paths' stores through a selected address and the whole Stream
+                // drops to scratch memory).
+                st.loop = 0.f;
+                st.move = 0.f;
+                st.seq = 0;
+                st.pos = 0;
+                st.endpos = 0;
+                st.rows_left = 0xFFFFFFFFu;
+                st.len = 0;
+#pragma unroll
+                for (int k = 0; k < S; ++k) st.M[k] = NINF;
+                st.J = NINF;
+                st.C = NINF;
+                st.N = 0.f;
+                st.B = 0.f;
+                st.active = false;
+                st.r0 = 0;
                 return;
             }
-            const uint32_t s = a.order ? a.order[cur] : cur;
+            const uint32_t s = a.order ? a.order[idx] : idx;
             const uint64_t o0 = a.offsets[s], o1 = a.offsets[s + 1];
             const uint64_t L = o1 - o0;
-            cur = nxt;
-            nxt = group_dequeue<G>(a.counter, leader, lane);
             if (L == 0) {  // empty record: the DP loop never runs, C_0 = -inf (MSV_HMM.cpp:86,112)
                 if (leader) a.scores[s] = NINF;
                 continue;
@@ -167,125 +201,126 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
                 continue;
             }
             const float2 lm = a.lentab[L];
-            loop = lm.x;
-            move = lm.y;
-            seq = s;
-            pos = static_cast<uint32_t>(o0);
-            endpos = static_cast<uint32_t>(o1 - 1);
-            rows_left = static_cast<uint32_t>(L);
+            st.loop = lm.x;
+            st.move = lm.y;
+            st.seq = s;
+            st.pos = static_cast<uint32_t>(o0);
+            st.endpos = static_cast<uint32_t>(o1 - 1);
+            st.rows_left = static_cast<uint32_t>(L);
+            st.len = static_cast<uint32_t>(L);
 #pragma unroll
-            for (int k = 0; k < S; ++k) M[k] = NINF;
-            J = NINF;
-            C = NINF;
-            N = 0.f;    // dp[0][N] = 0      (MSV_HMM.cpp:96)
-            B = move;   // dp[0][B] = tr_move (MSV_HMM.cpp:97)
-            active = true;
+            for (int k = 0; k < S; ++k) st.M[k] = NINF;
+            st.J = NINF;
+            st.C = NINF;
+            st.N = 0.f;       // dp[0][N] = 0      (MSV_HMM.cpp:96)
+            st.B = st.move;   // dp[0][B] = tr_move (MSV_HMM.cpp:97)
+            st.active = true;
+            st.r0 = res[st.pos];
             return;
         }
     };
+    auto init = [&](Stream<S>& st) {
+#pragma unroll
+        for (int k = 0; k < S; ++k) st.M[k] = NINF;
+        st.J = st.C = NINF;
+        st.N = st.B = st.loop = st.move = 0.f;
+        st.pos = st.endpos = st.seq = st.len = st.r0 = 0;
+        st.rows_left = 0xFFFFFFFFu;
+        st.active = false;
+        begin(st);
+    };
+    // Row prologue: next residue prefetch, emission row pointer, Bt, the j-1 neighbour, ring fill.
+    auto prologue = [&](Stream<S>& st, RowCtx<PF>& rc) {
+        rc.r1 = res[min(st.pos + 1, st.endpos)];  // next row's residue, one row of prefetch
+        const uint32_t rr = min(st.r0, static_cast<uint32_t>(kPoisonRow));
+        if constexpr (!BIG) {
+            rc.ep = &tab[rr * ROW_F4 + gl];
+        } else {
+            rc.ep = (rr < static_cast<uint32_t>(LDS_ROWS)) ? &tab[rr * ROW_F4 + gl] : &a.etab[rr * ROW_F4 + gl];
+        }
+        rc.Bt = st.B + trBMk;
+        rc.nbr = shift_in<G>(st.M[S - 1], NINF);
+        rc.p0 = NINF;
+        rc.p1 = NINF;
+        rc.p2 = NINF;
+        rc.p3 = NINF;
+#pragma unroll
+        for (int q = 0; q < PF; ++q) rc.ring[q] = rc.ep[(C4 - 1 - q) * G];
+    };
+    // One float4 chunk (states 4c+1 .. 4c+4 of the lane), highest state first so M[k-1] is still
+    // the previous row's value; the next chunk is requested PF chunks ahead.
+    auto chunk = [&](Stream<S>& st, RowCtx<PF>& rc, auto cc) {
+        constexpr int c = decltype(cc)::value;
+        constexpr int slot = (C4 - 1 - c) % PF;
+        const float4 ev = rc.ring[slot];
+        // (EXP & 1: timing-only experiment, emissions not re-read -> wrong scores, never shipped)
+        if constexpr (c - PF >= 0 && !(EXP & 1)) rc.ring[slot] = rc.ep[(c - PF) * G];
+        constexpr int k = 4 * c;
+        st.M[k + 3] = ev.w + fmaxf(st.M[k + 2], rc.Bt);
+        st.M[k + 2] = ev.z + fmaxf(st.M[k + 1], rc.Bt);
+        st.M[k + 1] = ev.y + fmaxf(st.M[k], rc.Bt);
+        if constexpr (c == 0) {
+            st.M[k] = ev.x + fmaxf(rc.nbr, rc.Bt);
+        } else {
+            st.M[k] = ev.x + fmaxf(st.M[k - 1], rc.Bt);
+        }
+        if constexpr ((EXP & 4) && (c & 1)) {  // 4 accumulators: half-length E dependency chains
+            rc.p2 = fmaxf(fmaxf(rc.p2, st.M[k + 3]), st.M[k + 2]);
+            rc.p3 = fmaxf(fmaxf(rc.p3, st.M[k + 1]), st.M[k]);
+        } else {
+            rc.p0 = fmaxf(fmaxf(rc.p0, st.M[k + 3]), st.M[k + 2]);
+            rc.p1 = fmaxf(fmaxf(rc.p1, st.M[k + 1]), st.M[k]);
+        }
+    };
+    // Row epilogue: E over the group, the specials (MSV_HMM.cpp:107-110), cursor advance.
+    auto epilogue = [&](Stream<S>& st, RowCtx<PF>& rc) {
+        const float Elane = (EXP & 4) ? fmaxf(fmaxf(rc.p0, rc.p1), fmaxf(rc.p2, rc.p3)) : fmaxf(rc.p0, rc.p1);
+        const float E = group_max<G>(Elane);
+        st.J = fmaxf(st.J + st.loop, E + tEJ);
+        st.C = fmaxf(st.C + st.loop, E + tEC);
+        st.N = st.N + st.loop;
+        st.B = fmaxf(st.N, st.J) + st.move;
+        ++st.pos;
+        --st.rows_left;
+        st.r0 = rc.r1;
+    };
+    auto finish = [&](Stream<S>& st) {
+        const float sc = st.C + st.move;  // dp.back()[C] + tr_move (MSV_HMM.cpp:112)
+        if (leader) {
+            a.scores[st.seq] = sc;
+            if (!(sc <= 3.402823466e38f)) atomicOr(a.errors, kErrBadResidue);  // poison row hit
+        }
+        begin(st);
+    };
 
-    begin();
-    uint32_t r0 = res[pos];
-    uint32_t r1 = res[min(pos + 1, endpos)];
+    // D independent sequences per lane group ("streams"): their rows interleave chunk by chunk,
+    // so one stream's serial per-row section (E butterfly -> J/C/N/B -> Bt) overlaps the other
+    // stream's cell updates inside the same wave.
+    Stream<S> s0, s1;
+    init(s0);
+    if constexpr (D == 2) init(s1);
+
     uint64_t t_start = 0;
     if (a.stamps) t_start = __builtin_amdgcn_s_memrealtime();
-    uint32_t rows_done = 0;
 
-    while (__any(active)) {
-        const uint32_t r2 = res[min(pos + 2, endpos)];
-        const uint32_t rr = min(r0, static_cast<uint32_t>(kPoisonRow));
-
-        const float4* ep;
-        if constexpr (!BIG) {
-            ep = &tab[rr * ROW_F4 + gl];
-        } else {
-            ep = (rr < static_cast<uint32_t>(LDS_ROWS)) ? &tab[rr * ROW_F4 + gl] : &a.etab[rr * ROW_F4 + gl];
-        }
-        const float Bt = B + trBMk;
-        const float nbr = shift_in<G>(M[S - 1], NINF);
-        float Elane;
-
-        if constexpr (PF == 0) {
-            // All S emissions in flight at once (S extra VGPRs), compiler-scheduled.
-            float4 e[C4];
-#pragma unroll
-            for (int c = 0; c < C4; ++c) e[c] = ep[c * G];
-            // Update in place from the highest state down, so M[k-1] is still the previous row.
-#pragma unroll
-            for (int k = S - 1; k >= 1; --k) {
-                const float4 ev = e[k >> 2];
-                const float ek = (k & 3) == 0 ? ev.x : (k & 3) == 1 ? ev.y : (k & 3) == 2 ? ev.z : ev.w;
-                M[k] = ek + fmaxf(M[k - 1], Bt);
-            }
-            M[0] = e[0].x + fmaxf(nbr, Bt);
-            // E = max_j M_j : four independent max3 chains
-            float p0 = M[0], p1 = M[1], p2 = M[2], p3 = M[3];
-#pragma unroll
-            for (int k = 4; k < S; k += 4) {
-                p0 = fmaxf(p0, M[k]);
-                p1 = fmaxf(p1, M[k + 1]);
-                p2 = fmaxf(p2, M[k + 2]);
-                p3 = fmaxf(p3, M[k + 3]);
-            }
-            Elane = fmaxf(fmaxf(p0, p1), fmaxf(p2, p3));
-        } else {
-            // Streamed: a ring of PF float4 chunks in flight, one chunk (4 states) consumed per
-            // step, scheduling pinned per chunk so only PF*4 emission VGPRs are live -> fewer
-            // VGPRs, more waves per SIMD to hide the per-row serial section.
-            float4 ring[PF];
-#pragma unroll
-            for (int d = 0; d < PF; ++d) ring[d] = ep[(C4 - 1 - d) * G];
-            float p0 = NINF, p1 = NINF;
-#pragma unroll
-            for (int c = C4 - 1; c >= 0; --c) {
-                const int slot = (C4 - 1 - c) % PF;
-                const float4 ev = ring[slot];
-                if (c - PF >= 0) ring[slot] = ep[(c - PF) * G];
-                const int k = 4 * c;
-                M[k + 3] = ev.w + fmaxf(M[k + 2], Bt);
-                M[k + 2] = ev.z + fmaxf(M[k + 1], Bt);
-                M[k + 1] = ev.y + fmaxf(M[k], Bt);
-                M[k] = ev.x + fmaxf(c == 0 ? nbr : M[k - 1], Bt);
-                p0 = fmaxf(fmaxf(p0, M[k + 3]), M[k + 2]);
-                p1 = fmaxf(fmaxf(p1, M[k + 1]), M[k]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            Elane = fmaxf(p0, p1);
-        }
-        const float E = group_max<G>(Elane);
-
-        J = fmaxf(J + loop, E + tEJ);
-        C = fmaxf(C + loop, E + tEC);
-        N = N + loop;
-        B = fmaxf(N, J) + move;
-
-        ++pos;
-        --rows_left;
-        r0 = r1;
-        r1 = r2;
-        if (rows_left == 0) {
-            const float sc = C + move;  // dp.back()[C] + tr_move (MSV_HMM.cpp:112)
-            if (leader) {
-                a.scores[seq] = sc;
-                if (!(sc <= 3.402823466e38f)) atomicOr(a.errors, kErrBadResidue);  // poison row hit
-            }
-            begin();
-            r0 = res[pos];
-            r1 = res[min(pos + 1, endpos)];
+    while (__any(D == 2 ? (s0.active || s1.active) : s0.active)) {
+        RowCtx<PF> c0, c1;
+        prologue(s0, c0);
+        if constexpr (D == 2) prologue(s1, c1);
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+            // chunks C4-1 .. 0, each step pinned so only the rings' registers are live
+            ((chunk(s0, c0, std::integral_constant<int, C4 - 1 - I>{}),
+              [&] { if constexpr (D == 2) chunk(s1, c1, std::integral_constant<int, C4 - 1 - I>{}); }(),
+              [&] { if constexpr (!(EXP & 2) || (I & 1)) __builtin_amdgcn_sched_barrier(0); }()),
+             ...);
+        }(std::make_integer_sequence<int, C4>{});
+        epilogue(s0, c0);
+        if constexpr (D == 2) epilogue(s1, c1);
+        if (s0.rows_left == 0) finish(s0);
+        if constexpr (D == 2) {
+            if (s1.rows_left == 0) finish(s1);
         }
         ++rows_done;
-        // Rotate issue priority among the waves sharing a SIMD (waves w, w+4, w+8, w+12 of the
-        // workgroup): VALU issue is arbitrated by priority, then age, so without this the oldest
-        // wave runs ~2.5x faster than the youngest and the slow waves' last sequences form a long
-        // tail after the queue drains.  Rotation equalises their progress.
-        if (a.prio_shift && (rows_done & ((1u << a.prio_shift) - 1)) == 0) {
-            switch (((rows_done >> a.prio_shift) + (threadIdx.x >> 8)) & 3) {
-                case 0: __builtin_amdgcn_s_setprio(0); break;
-                case 1: __builtin_amdgcn_s_setprio(1); break;
-                case 2: __builtin_amdgcn_s_setprio(2); break;
-                default: __builtin_amdgcn_s_setprio(3); break;
-            }
-        }
     }
     // Diagnostic only (a.stamps == nullptr in production): per-wave start/end realtime (100 MHz),
     // rows issued, XCC id.  Never read by the kernel; used by tools/wave_timeline.py.
@@ -378,14 +413,26 @@ __global__ __launch_bounds__(kOrderThreads) void order_place_kernel(const uint64
 // covers LENG with the least estimated cost (the analog of the reference's should_specialize,
 // which bakes sizes into the OpenCL program with -D defines, MSV_HMM.cpp:322-337).
 // ------------------------------------------------------------------------------------------------
-#define MSV_VARIANT(G_, S_, W_, P_)                                                                       \
-    Variant{G_, S_, W_, P_, lds_rows_for(G_, S_), lds_rows_for(G_, S_) < kTableRows,                      \
+#define MSV_VARIANT(G_, S_, W_, P_, D_)                                                                   \
+    Variant{G_, S_, W_, P_, D_, lds_rows_for(G_, S_), lds_rows_for(G_, S_) < kTableRows,                  \
             reinterpret_cast<const void*>(                                                                 \
-                &msv_batch_kernel<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows)>),                   \
-            "msv_g" #G_ "_s" #S_ "_w" #W_ "_p" #P_}
+                &msv_batch_kernel<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_>),               \
+            "msv_g" #G_ "_s" #S_ "_w" #W_ "_p" #P_ "_d" #D_}
+
+#define MSV_EXPERIMENT(G_, S_, W_, P_, D_, X_)                                                            \
+    Variant{G_, S_, W_, P_, D_, lds_rows_for(G_, S_), lds_rows_for(G_, S_) < kTableRows,                  \
+            reinterpret_cast<const void*>(                                                                 \
+                &msv_batch_kernel<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_, X_>),           \
+            "exp" #X_ "_g" #G_ "_s" #S_ "_w" #W_ "_p" #P_ "_d" #D_}
 
 static const Variant kVariants[] = {
 #include "msv_variants.inc"
+    // timing-only experiments (wrong scores by construction; selected only by name in tools/)
+    MSV_EXPERIMENT(16, 88, 16, 2, 1, 1),
+    MSV_EXPERIMENT(16, 88, 16, 4, 1, 2),
+    MSV_EXPERIMENT(16, 88, 16, 2, 1, 4),
+    MSV_EXPERIMENT(16, 88, 16, 4, 1, 6),
+    MSV_EXPERIMENT(16, 88, 16, 3, 1, 4),
 };
 
 const Variant* variants(int* count) {

@@ -20,7 +20,8 @@ def main():
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--variant", default="")
     ap.add_argument("--no-order", action="store_true")
-    ap.add_argument("--prio-shift", type=int, default=-1)
+
+
     args = ap.parse_args()
     import torch
     import hmm_fasta_viterbi_amd as msv
@@ -35,9 +36,8 @@ def main():
     eng = msv.MSV_HMM(msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof)))
     if args.variant:
         eng.set_variant(args.variant)
-    if args.prio_shift >= 0:
-        L.msv_debug_set_prio_shift.argtypes = [C.c_void_p, C.c_uint32]
-        L.msv_debug_set_prio_shift(eng._p, args.prio_shift)
+
+
     codes, offsets = random_batch(seed * 1000, n, lmin, lmax)
     dev = torch.device("cuda:0")
     st = torch.cuda.Stream(dev)
@@ -77,7 +77,7 @@ def main():
         "end_by_wave_in_block_median": [round(float(np.median(end[wid == w])), 0) for w in range(W)],
     }
     res = {
-        "variant": eng.describe()["variant"], "order": not args.no_order, "prio_shift": args.prio_shift, "waves": int(len(a)),
+        "variant": eng.describe()["variant"], "order": not args.no_order,  "waves": int(len(a)),
         "launch_us": round(float(T), 1),
         "start_us_pct": q(start), "end_us_pct": q(end),
         "mean_wave_lifetime_frac": round(float(life.mean()), 4),
