@@ -103,10 +103,14 @@ __device__ __forceinline__ uint32_t group_bcast(uint32_t v, int lane) {
 }
 
 // Next sequence index for the whole group (one atomic by the group leader, broadcast).
+// Branch-free on purpose: with `if (leader) v = atomicAdd(...)` the ROCm 7.2 optimiser unswitched
+// a loop containing this on `leader` into per-lane copies; the non-leader copy lost the atomic and
+// its ds_bpermute read a lane that was not executing (a launch that spun forever on index 0).
+// Every lane issues the atomic with increment leader ? 1 : 0; the wave-level atomic optimiser turns
+// that into one atomic per wave.
 template <int G>
 __device__ __forceinline__ uint32_t group_take(uint32_t* counter, bool leader, int lane) {
-    uint32_t v = 0;
-    if (leader) v = atomicAdd(counter, 1u);
+    const uint32_t v = atomicAdd(counter, leader ? 1u : 0u);
     return group_bcast<G>(v, lane);
 }
 
@@ -115,12 +119,22 @@ __device__ __forceinline__ uint32_t group_take(uint32_t* counter, bool leader, i
 // Per-lane state of one sequence being scored (one "stream"): S match states of the DP row in
 // VGPRs, the specials, and the residue cursor.  Separate objects (never an indexed array) so all of
 // it stays in registers.
+// Rows of residue prefetch: a row of a small profile is short (S=8: ~45 VALU), so the byte load
+// for a row is issued RPF rows ahead to cover the L2/HBM latency.
+template <int S>
+constexpr int residue_prefetch() {
+    return S <= 16 ? 6 : (S <= 40 ? 3 : 1);
+}
+
 template <int S>
 struct Stream {
+    static constexpr int RPF = residue_prefetch<S>();
     float M[S];
     float J, C, N, B, loop, move;
-    uint32_t pos, endpos, rows_left, seq, len, r0;  // r0 = residue code of the next row (prefetched)
+    uint32_t pos, endpos, rows_left, seq, half;  // half: rows_left at which to fetch the next index
+    uint32_t r[RPF];  // residue codes of the next RPF rows (r[0] = this row)
     bool active;
+    bool junk;        // current "sequence" is an empty/too-long record: discard its row
 };
 
 // Per-row working set of one stream.
@@ -128,7 +142,7 @@ template <int PF>
 struct RowCtx {
     const float4* ep;
     float Bt, nbr, p0, p1, p2, p3;
-    uint32_t r1;
+    uint32_t rnext;  // residue code RPF rows ahead
     float4 ring[PF];
 };
 
@@ -155,84 +169,64 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     const float trBMk = a.tr_B_Mk, tEC = a.tr_E_C, tEJ = a.tr_E_J;
 
     uint32_t rows_done = 0;  // rows issued by this wave (diagnostics)
-    // Sequence indices are prefetched one ahead (the atomic's latency hides behind a sequence).
-    uint32_t cur = group_take<G>(a.counter, leader, lane);
-    uint32_t nxt = group_take<G>(a.counter, leader, lane);
+    // Work distribution: a group takes its first sequence when it starts; the index of its next
+    // sequence is fetched when the current one is half done (so the atomic's latency hides behind
+    // half a sequence, and a batch smaller than twice the number of groups is still spread one
+    // sequence per group instead of two per early group).
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    uint32_t pending = kNone;
 
     // Start the next non-empty sequence in a stream (or retire the stream).
     auto begin = [&](Stream<S>& st) {
-        for (;;) {
-            const uint32_t idx = cur;
-            cur = nxt;
-            nxt = group_take<G>(a.counter, leader, lane);
-            if (idx >= a.n) {
-                // Retire: assign exactly the fields the start path assigns (otherwise the compiler
-                // merges the two paths' stores through a selected address and the whole Stream
-                // drops to scratch memory).
-                st.loop = 0.f;
-                st.move = 0.f;
-                st.seq = 0;
-                st.pos = 0;
-                st.endpos = 0;
-                st.rows_left = 0xFFFFFFFFu;
-                st.len = 0;
-#pragma unroll
-                for (int k = 0; k < S; ++k) st.M[k] = NINF;
-                st.J = NINF;
-                st.C = NINF;
-                st.N = 0.f;
-                st.B = 0.f;
-                st.active = false;
-                st.r0 = 0;
-                return;
-            }
-            const uint32_t s = a.order ? a.order[idx] : idx;
-            const uint64_t o0 = a.offsets[s], o1 = a.offsets[s + 1];
-            const uint64_t L = o1 - o0;
-            if (L == 0) {  // empty record: the DP loop never runs, C_0 = -inf (MSV_HMM.cpp:86,112)
-                if (leader) a.scores[s] = NINF;
-                continue;
-            }
-            if (L >= a.lentab_n) {
-                if (leader) {
-                    a.scores[s] = __uint_as_float(0x7fc00000u);  // quiet NaN bits
-                    atomicOr(a.errors, kErrTooLong);
-                }
-                continue;
-            }
-            const float2 lm = a.lentab[L];
-            st.loop = lm.x;
-            st.move = lm.y;
-            st.seq = s;
-            st.pos = static_cast<uint32_t>(o0);
-            st.endpos = static_cast<uint32_t>(o1 - 1);
-            st.rows_left = static_cast<uint32_t>(L);
-            st.len = static_cast<uint32_t>(L);
-#pragma unroll
-            for (int k = 0; k < S; ++k) st.M[k] = NINF;
-            st.J = NINF;
-            st.C = NINF;
-            st.N = 0.f;       // dp[0][N] = 0      (MSV_HMM.cpp:96)
-            st.B = st.move;   // dp[0][B] = tr_move (MSV_HMM.cpp:97)
-            st.active = true;
-            st.r0 = res[st.pos];
-            return;
+        // Loop-free on purpose: a retry loop around the group broadcast here was unswitched by
+        // the compiler into per-lane copies (see group_take).  An empty (or too long) record
+        // instead becomes a one-row "junk" stream: its score is written now, one row is computed
+        // on neutral state and discarded, and the stream then restarts with the next index.
+        uint32_t idx = pending;
+        pending = kNone;
+        if (idx == kNone) idx = group_take<G>(a.counter, leader, lane);
+        const bool retire = idx >= a.n;
+        uint32_t s = 0;
+        uint64_t o0 = 0, o1 = 0;
+        if (!retire) {
+            s = a.order ? a.order[idx] : idx;
+            o0 = a.offsets[s];
+            o1 = a.offsets[s + 1];
         }
-    };
-    auto init = [&](Stream<S>& st) {
+        const uint64_t L = o1 - o0;
+        const bool empty = !retire && L == 0;            // C_0 = -inf (MSV_HMM.cpp:86,112)
+        const bool too_long = !retire && L >= a.lentab_n;
+        if (leader && empty) a.scores[s] = NINF;
+        if (leader && too_long) {
+            a.scores[s] = __uint_as_float(0x7fc00000u);  // quiet NaN bits
+            atomicOr(a.errors, kErrTooLong);
+        }
+        const bool run = !retire && !empty && !too_long;
+        const float2 lm = run ? a.lentab[L] : make_float2(0.f, 0.f);
+        st.loop = lm.x;
+        st.move = lm.y;
+        st.seq = s;
+        st.pos = run ? static_cast<uint32_t>(o0) : 0u;
+        st.endpos = run ? static_cast<uint32_t>(o1 - 1) : 0u;
+        st.rows_left = retire ? 0xFFFFFFFFu : (run ? static_cast<uint32_t>(L) : 1u);
+        // half == 0xFFFFFFFF equals the initial rows_left of a retired stream: never matched again
+        st.half = run ? static_cast<uint32_t>(L >> 1) : 0xFFFFFFFFu;
 #pragma unroll
         for (int k = 0; k < S; ++k) st.M[k] = NINF;
-        st.J = st.C = NINF;
-        st.N = st.B = st.loop = st.move = 0.f;
-        st.pos = st.endpos = st.seq = st.len = st.r0 = 0;
-        st.rows_left = 0xFFFFFFFFu;
-        st.active = false;
-        begin(st);
+        st.J = NINF;
+        st.C = NINF;
+        st.N = 0.f;       // dp[0][N] = 0      (MSV_HMM.cpp:96)
+        st.B = st.move;   // dp[0][B] = tr_move (MSV_HMM.cpp:97)
+        st.active = !retire;
+        st.junk = !run;
+#pragma unroll
+        for (int q = 0; q < Stream<S>::RPF; ++q) st.r[q] = res[min(st.pos + q, st.endpos)];
     };
+    auto init = [&](Stream<S>& st) { begin(st); };
     // Row prologue: next residue prefetch, emission row pointer, Bt, the j-1 neighbour, ring fill.
     auto prologue = [&](Stream<S>& st, RowCtx<PF>& rc) {
-        rc.r1 = res[min(st.pos + 1, st.endpos)];  // next row's residue, one row of prefetch
-        const uint32_t rr = min(st.r0, static_cast<uint32_t>(kPoisonRow));
+        rc.rnext = res[min(st.pos + Stream<S>::RPF, st.endpos)];
+        const uint32_t rr = min(st.r[0], static_cast<uint32_t>(kPoisonRow));
         if constexpr (!BIG) {
             rc.ep = &tab[rr * ROW_F4 + gl];
         } else {
@@ -282,11 +276,13 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         st.B = fmaxf(st.N, st.J) + st.move;
         ++st.pos;
         --st.rows_left;
-        st.r0 = rc.r1;
+#pragma unroll
+        for (int q = 0; q + 1 < Stream<S>::RPF; ++q) st.r[q] = st.r[q + 1];
+        st.r[Stream<S>::RPF - 1] = rc.rnext;
     };
     auto finish = [&](Stream<S>& st) {
         const float sc = st.C + st.move;  // dp.back()[C] + tr_move (MSV_HMM.cpp:112)
-        if (leader) {
+        if (leader && !st.junk) {
             a.scores[st.seq] = sc;
             if (!(sc <= 3.402823466e38f)) atomicOr(a.errors, kErrBadResidue);  // poison row hit
         }
@@ -316,6 +312,10 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         }(std::make_integer_sequence<int, C4>{});
         epilogue(s0, c0);
         if constexpr (D == 2) epilogue(s1, c1);
+        if (s0.rows_left == s0.half && pending == kNone) pending = group_take<G>(a.counter, leader, lane);
+        if constexpr (D == 2) {
+            if (s1.rows_left == s1.half && pending == kNone) pending = group_take<G>(a.counter, leader, lane);
+        }
         if (s0.rows_left == 0) finish(s0);
         if constexpr (D == 2) {
             if (s1.rows_left == 0) finish(s1);
@@ -327,11 +327,12 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     if (a.stamps && lane == 0) {
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
         const uint32_t w = blockIdx.x * WAVES + (threadIdx.x >> 6);
-        uint32_t xcc = 0;
+        uint32_t xcc = 0, hwid = 0;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
         a.stamps[4 * w + 0] = t_start;
         a.stamps[4 * w + 1] = t_end;
-        a.stamps[4 * w + 2] = rows_done;
+        a.stamps[4 * w + 2] = (static_cast<uint64_t>(hwid) << 32) | rows_done;
         a.stamps[4 * w + 3] = (static_cast<uint64_t>(xcc) << 32) | blockIdx.x;
     }
 }

@@ -18,6 +18,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg3")
+    ap.add_argument("--n", type=int, default=0)
     ap.add_argument("--variant", default="")
     ap.add_argument("--no-order", action="store_true")
 
@@ -33,6 +34,7 @@ def main():
     L.msv_debug_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
     L.msv_debug_grid_waves.argtypes = [C.c_void_p]
     prof, n, lmin, lmax, seed = CONFIGS[args.config]
+    n = args.n or n
     eng = msv.MSV_HMM(msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof)))
     if args.variant:
         eng.set_variant(args.variant)
@@ -62,7 +64,12 @@ def main():
     start = (a[:, 0] - t0) / 100.0  # us
     end = (a[:, 1] - t0) / 100.0
     T = end.max()
-    rows = a[:, 2].astype(np.float64)
+    rows = (a[:, 2] & 0xFFFFFFFF).astype(np.float64)
+    hwid = (a[:, 2] >> 32).astype(np.int64)
+    cu_key = (a[:, 3] >> 32).astype(np.int64) * 4096 + ((hwid >> 8) & 0xF) + 16 * ((hwid >> 12) & 0x1) + \
+        32 * ((hwid >> 13) & 0x7)
+    simd = (hwid >> 4) & 0x3
+    _, waves_per_cu = np.unique(cu_key, return_counts=True)
     xcc = (a[:, 3] >> 32).astype(int)
     life = (end - start) / T
     q = lambda x: [round(float(np.percentile(x, p)), 1) for p in (0, 1, 10, 50, 90, 99, 100)]
@@ -73,6 +80,9 @@ def main():
     idx = np.nonzero(stamps.cpu().numpy().reshape(nw, 4)[:, 1] > 0)[0]
     wid = idx % W
     res_extra = {
+        "distinct_cus": int(len(waves_per_cu)),
+        "waves_per_cu_pct": q(waves_per_cu),
+        "simd_of_wave_in_block": [int(np.bincount(simd[wid == w], minlength=4).argmax()) for w in range(W)],
         "rows_by_wave_in_block_median": [int(np.median(rows[wid == w])) for w in range(W)],
         "end_by_wave_in_block_median": [round(float(np.median(end[wid == w])), 0) for w in range(W)],
     }
