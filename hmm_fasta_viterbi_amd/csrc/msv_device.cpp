@@ -80,9 +80,13 @@ msv_status hip_status(hipError_t e) {
     } while (0)
 
 // Estimated issue cost of one row for one sequence: 2.5 VALU per state-slot plus the per-row
-// specials/reduction, times the lanes a sequence occupies.
+// specials/reduction, times the lanes a sequence occupies.  A BIG table costs little with one
+// sequence per wave (G = 64: wave-uniform LDS/L2 row split) and a lot with 2-4 sequences per wave
+// (generic loads with per-lane address selects); measured on 2405.hmm: 7.4 vs 10.5 ms.
 double variant_cost(const msvk::Variant& v) {
-    return (2.5 * v.S + 26.0) * v.G * (v.big ? 1.6 : 1.0) * (v.pf == 2 ? 1.0 : 1.05) * (v.streams == 2 ? 1.15 : 1.0);
+    const double big = !v.big ? 1.0 : (v.G == 64 ? 1.03 : 1.6);
+    const double row = v.G == 64 ? 36.0 : 26.0;  // + permlane32 step, scalar sequence bookkeeping
+    return (2.5 * v.S + row) * v.G * big * (v.pf == 2 ? 1.0 : 1.05) * (v.streams == 2 ? 1.15 : 1.0);
 }
 
 const msvk::Variant* pick_variant(uint32_t states) {
@@ -92,6 +96,7 @@ const msvk::Variant* pick_variant(uint32_t states) {
     for (int i = 0; i < count; ++i) {
         const msvk::Variant& v = all[i];
         if (static_cast<uint32_t>(v.G * v.S) < states) continue;
+        if (std::strncmp(v.name, "exp", 3) == 0) continue;  // timing-only experiments
         if (!best || variant_cost(v) < variant_cost(*best)) best = &v;
     }
     return best;

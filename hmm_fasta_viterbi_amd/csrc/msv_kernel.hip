@@ -68,11 +68,14 @@ template <int G>
 __device__ __forceinline__ float shift_in(float last, float ninf) {
     if constexpr (G == 16) {
         return dpp<DPP_ROW_SHR1>(ninf, last);
-    } else {
-        static_assert(G == 32, "G must be 16 or 32");
+    } else if constexpr (G == 32) {
         // rows 1 and 3 first receive lane 15 of rows 0 and 2; row_shr:1 then fills every lane
         // except the first of each row, which keeps that broadcast (or -inf for rows 0 and 2).
         float v = dpp<DPP_ROW_BCAST15, 0xA>(ninf, last);
+        return dpp<DPP_ROW_SHR1>(v, last);
+    } else {
+        static_assert(G == 64, "G must be 16, 32 or 64");
+        float v = dpp<DPP_ROW_BCAST15, 0xE>(ninf, last);  // rows 1-3 get lane 15 of the row before
         return dpp<DPP_ROW_SHR1>(v, last);
     }
 }
@@ -90,8 +93,12 @@ __device__ __forceinline__ float group_max(float x) {
     x = fmaxf(x, dpp_perm<DPP_QUAD_2301>(x));
     x = fmaxf(x, dpp_perm<DPP_ROW_HMIRROR>(x));
     x = fmaxf(x, dpp_perm<DPP_ROW_MIRROR>(x));
-    if constexpr (G == 32) {
+    if constexpr (G >= 32) {
         auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        x = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+    }
+    if constexpr (G == 64) {
+        auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
         x = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
     }
     return x;
@@ -140,6 +147,7 @@ struct Stream {
 // Per-row working set of one stream.
 template <int PF>
 struct RowCtx {
+    static constexpr int kPF = PF;
     const float4* ep;
     float Bt, nbr, p0, p1, p2, p3;
     uint32_t rnext;  // residue code RPF rows ahead
@@ -224,14 +232,18 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     };
     auto init = [&](Stream<S>& st) { begin(st); };
     // Row prologue: next residue prefetch, emission row pointer, Bt, the j-1 neighbour, ring fill.
-    auto prologue = [&](Stream<S>& st, RowCtx<PF>& rc) {
-        rc.rnext = res[min(st.pos + Stream<S>::RPF, st.endpos)];
+    auto row_ptr = [&](Stream<S>& st) -> const float4* {
         const uint32_t rr = min(st.r[0], static_cast<uint32_t>(kPoisonRow));
         if constexpr (!BIG) {
-            rc.ep = &tab[rr * ROW_F4 + gl];
+            return &tab[rr * ROW_F4 + gl];
         } else {
-            rc.ep = (rr < static_cast<uint32_t>(LDS_ROWS)) ? &tab[rr * ROW_F4 + gl] : &a.etab[rr * ROW_F4 + gl];
+            return (rr < static_cast<uint32_t>(LDS_ROWS)) ? &tab[rr * ROW_F4 + gl] : &a.etab[rr * ROW_F4 + gl];
         }
+    };
+    auto prologue = [&](Stream<S>& st, auto& rc, const float4* ep) {
+        constexpr int P = std::decay_t<decltype(rc)>::kPF;
+        rc.rnext = res[min(st.pos + Stream<S>::RPF, st.endpos)];
+        rc.ep = ep;
         rc.Bt = st.B + trBMk;
         rc.nbr = shift_in<G>(st.M[S - 1], NINF);
         rc.p0 = NINF;
@@ -239,16 +251,17 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         rc.p2 = NINF;
         rc.p3 = NINF;
 #pragma unroll
-        for (int q = 0; q < PF; ++q) rc.ring[q] = rc.ep[(C4 - 1 - q) * G];
+        for (int q = 0; q < P; ++q) rc.ring[q] = rc.ep[(C4 - 1 - q) * G];
     };
     // One float4 chunk (states 4c+1 .. 4c+4 of the lane), highest state first so M[k-1] is still
     // the previous row's value; the next chunk is requested PF chunks ahead.
-    auto chunk = [&](Stream<S>& st, RowCtx<PF>& rc, auto cc) {
+    auto chunk = [&](Stream<S>& st, auto& rc, auto cc) {
+        constexpr int P = std::decay_t<decltype(rc)>::kPF;
         constexpr int c = decltype(cc)::value;
-        constexpr int slot = (C4 - 1 - c) % PF;
+        constexpr int slot = (C4 - 1 - c) % P;
         const float4 ev = rc.ring[slot];
         // (EXP & 1: timing-only experiment, emissions not re-read -> wrong scores, never shipped)
-        if constexpr (c - PF >= 0 && !(EXP & 1)) rc.ring[slot] = rc.ep[(c - PF) * G];
+        if constexpr (c - P >= 0 && !(EXP & 1)) rc.ring[slot] = rc.ep[(c - P) * G];
         constexpr int k = 4 * c;
         st.M[k + 3] = ev.w + fmaxf(st.M[k + 2], rc.Bt);
         st.M[k + 2] = ev.z + fmaxf(st.M[k + 1], rc.Bt);
@@ -267,7 +280,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         }
     };
     // Row epilogue: E over the group, the specials (MSV_HMM.cpp:107-110), cursor advance.
-    auto epilogue = [&](Stream<S>& st, RowCtx<PF>& rc) {
+    auto epilogue = [&](Stream<S>& st, auto& rc) {
         const float Elane = (EXP & 4) ? fmaxf(fmaxf(rc.p0, rc.p1), fmaxf(rc.p2, rc.p3)) : fmaxf(rc.p0, rc.p1);
         const float E = group_max<G>(Elane);
         st.J = fmaxf(st.J + st.loop, E + tEJ);
@@ -299,19 +312,50 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     uint64_t t_start = 0;
     if (a.stamps) t_start = __builtin_amdgcn_s_memrealtime();
 
-    while (__any(D == 2 ? (s0.active || s1.active) : s0.active)) {
-        RowCtx<PF> c0, c1;
-        prologue(s0, c0);
-        if constexpr (D == 2) prologue(s1, c1);
+    // All chunks of one row, C4-1 .. 0, each step pinned so only the rings' registers are live.
+    auto row = [&](Stream<S>& st, auto& rc, const float4* ep) {
+        prologue(st, rc, ep);
         [&]<int... I>(std::integer_sequence<int, I...>) {
-            // chunks C4-1 .. 0, each step pinned so only the rings' registers are live
-            ((chunk(s0, c0, std::integral_constant<int, C4 - 1 - I>{}),
-              [&] { if constexpr (D == 2) chunk(s1, c1, std::integral_constant<int, C4 - 1 - I>{}); }(),
+            ((chunk(st, rc, std::integral_constant<int, C4 - 1 - I>{}),
               [&] { if constexpr (!(EXP & 2) || (I & 1)) __builtin_amdgcn_sched_barrier(0); }()),
              ...);
         }(std::make_integer_sequence<int, C4>{});
-        epilogue(s0, c0);
-        if constexpr (D == 2) epilogue(s1, c1);
+        epilogue(st, rc);
+    };
+
+    while (__any(D == 2 ? (s0.active || s1.active) : s0.active)) {
+        if constexpr (BIG && G == 64) {
+            // One sequence per wave: the residue, hence the table row's home, is wave-uniform, so
+            // the LDS rows and the L2 rows run as two separate (scalar-branched) row bodies with
+            // precise waits -- no generic loads, no per-lane selects.  An L2 row requests up to 10
+            // chunks up front to pay the L2 latency about once per row.
+            const uint32_t rr =
+                __builtin_amdgcn_readfirstlane(min(s0.r[0], static_cast<uint32_t>(kPoisonRow)));
+            // (EXP & 8: timing-only, every row served from LDS -> wrong scores; EXP & 16: L2 rows
+            // with the LDS ring depth)
+            if ((EXP & 8) || rr < static_cast<uint32_t>(LDS_ROWS)) {
+                RowCtx<PF> c0;
+                row(s0, c0, &tab[((EXP & 8) ? rr % LDS_ROWS : rr) * ROW_F4 + gl]);
+            } else {
+                RowCtx<(EXP & 16) ? PF : (C4 < 10 ? C4 : 10)> c0;
+                row(s0, c0, &a.etab[rr * ROW_F4 + gl]);
+            }
+        } else if constexpr (D == 1) {
+            RowCtx<PF> c0;
+            row(s0, c0, row_ptr(s0));
+        } else {
+            RowCtx<PF> c0, c1;
+            prologue(s0, c0, row_ptr(s0));
+            prologue(s1, c1, row_ptr(s1));
+            [&]<int... I>(std::integer_sequence<int, I...>) {
+                ((chunk(s0, c0, std::integral_constant<int, C4 - 1 - I>{}),
+                  chunk(s1, c1, std::integral_constant<int, C4 - 1 - I>{}),
+                  [&] { if constexpr (!(EXP & 2) || (I & 1)) __builtin_amdgcn_sched_barrier(0); }()),
+                 ...);
+            }(std::make_integer_sequence<int, C4>{});
+            epilogue(s0, c0);
+            epilogue(s1, c1);
+        }
         if (s0.rows_left == s0.half && pending == kNone) pending = group_take<G>(a.counter, leader, lane);
         if constexpr (D == 2) {
             if (s1.rows_left == s1.half && pending == kNone) pending = group_take<G>(a.counter, leader, lane);
@@ -434,6 +478,7 @@ static const Variant kVariants[] = {
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 4),
     MSV_EXPERIMENT(16, 88, 16, 4, 1, 6),
     MSV_EXPERIMENT(16, 88, 16, 3, 1, 4),
+    MSV_EXPERIMENT(64, 40, 16, 2, 1, 8),
 };
 
 const Variant* variants(int* count) {

@@ -34,3 +34,41 @@ def write_fasta(path: str, codes: np.ndarray, offsets: np.ndarray, line: int = 7
             s = letters[int(offsets[i]):int(offsets[i + 1])]
             for k in range(0, len(s), line):
                 f.write(s[k:k + line] + "\n")
+
+
+def write_hmm(path: str, leng: int, seed: int) -> None:
+    """A seeded HMMER3/b text profile of LENG `leng` (random -log probabilities in the ranges
+    real Pfam profiles use), for model lengths beyond the reference's data/ set (max 2405).
+    Layout as data/profile_HMMs/*.hmm: header tags, STATS LOCAL lines, COMPO block, then per node
+    a match-emission line, an insert-emission line and a 7-field transition line ('*' = p 1)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+
+    def row(vals):
+        return "".join(f"  {v:7.5f}" if v is not None else "        *" for v in vals)
+
+    out = [
+        "HMMER3/b [synthetic]",
+        f"NAME  synthetic_{leng}_{seed}",
+        f"LENG  {leng}",
+        "ALPH  amino",
+        "STATS LOCAL MSV       -9.9000  0.70000",
+        "STATS LOCAL VITERBI  -10.5000  0.70000",
+        "STATS LOCAL FORWARD   -4.0000  0.70000",
+        "HMM     " + "".join(f"     {a}   " for a in AMINO_ACIDS),
+        "            m->m     m->i     m->d     i->m     i->i     d->m     d->d",
+    ]
+    ins = rng.uniform(2.3, 4.5, 20)
+    out.append("  COMPO " + row(rng.uniform(2.3, 4.5, 20)))
+    out.append("        " + row(ins))
+    out.append("        " + row([0.05, 4.1, 3.0, 0.62, 0.77, 0.0, None]))
+    for k in range(1, leng + 1):
+        out.append(f"{k:7d} " + row(rng.uniform(0.5, 5.5, 20)))
+        out.append("        " + row(ins))
+        last = k == leng
+        out.append("        " + row([rng.uniform(0.01, 0.1), rng.uniform(3.5, 5.0),
+                                     None if last else rng.uniform(4.0, 6.0), 0.62, 0.77,
+                                     0.0 if last else rng.uniform(0.3, 0.6),
+                                     None if last else rng.uniform(0.8, 1.2)]))
+    out.append("//")
+    with open(path, "w") as f:
+        f.write("\n".join(out) + "\n")

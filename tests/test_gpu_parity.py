@@ -183,3 +183,52 @@ def test_describe_variant_for_1400():
     d = engine("1400.hmm").describe()
     assert d["model_length"] == 1401
     assert d["lanes_per_group"] * d["states_per_lane"] >= 1400
+
+
+
+def _variant_shape(name):
+    parts = name.split("_")
+    return int(parts[1][1:]), int(parts[2][1:])
+
+
+def test_every_variant_matches_oracle(tmp_path):
+    """Every shipped kernel instantiation (G, S, waves, PF, D), forced with set_variant, on the
+    largest profile it covers (so BIG variants run a real BIG table), against the oracle.  Model
+    lengths past the reference's largest profile (2405) use seeded synthetic HMMER3 files."""
+    from hmm_fasta_viterbi_amd.synthetic import write_hmm
+    paths = [profile_path(p) for p in PROFILES]
+    for leng in (2600, 3000, 3500, 4096):
+        paths.append(str(tmp_path / f"syn{leng}.hmm"))
+        write_hmm(paths[-1], leng, leng)
+    lengs = {p: msv.Profile_HMM(p).model_length - 1 for p in paths}
+    codes, offsets = random_batch(21, 48, 0, 400)
+    by_prof = {}
+    for name in msv.MSV_HMM.variants():
+        if name.startswith("exp"):
+            continue
+        g, s = _variant_shape(name)
+        fits = [p for p in paths if lengs[p] <= g * s]
+        if fits:
+            by_prof.setdefault(max(fits, key=lambda p: lengs[p]), []).append(name)
+    assert sum(len(v) for v in by_prof.values()) >= 40
+    for prof, names in by_prof.items():
+        want = OracleProfile(prof).score_batch(codes, offsets)
+        e = msv.MSV_HMM(msv.Profile_HMM(prof))
+        for name in names:
+            e.set_variant(name)
+            got = e.score_batch(codes=codes, offsets=offsets)
+            assert np.array_equal(bits(got), bits(want)), (prof, name)
+        e.close()
+
+
+def test_synthetic_4096_auto_variant(tmp_path):
+    """The largest supported model (4096 states) under the automatic variant choice, at the cfg5
+    sequence-length range."""
+    from hmm_fasta_viterbi_amd.synthetic import write_hmm
+    path = str(tmp_path / "syn4096.hmm")
+    write_hmm(path, 4096, 1)
+    codes, offsets = random_batch(5, 40, 1500, 2500)
+    e = msv.MSV_HMM(msv.Profile_HMM(path))
+    assert e.describe()["lanes_per_group"] == 64
+    assert np.array_equal(bits(e.score_batch(codes=codes, offsets=offsets)),
+                          bits(OracleProfile(path).score_batch(codes, offsets)))

@@ -115,6 +115,21 @@ def test_msv_precompute_matches_oracle():
         assert bits([b, c, j]).tolist() == bits(o.constants()).tolist()
 
 
+def test_synthetic_profile_writer_parses_like_oracle(tmp_path):
+    """synthetic.write_hmm (models beyond the reference's 2405 states): the product parser and the
+    oracle parser agree on every array and on the MSV precompute."""
+    from hmm_fasta_viterbi_amd.synthetic import write_hmm
+    path = str(tmp_path / "syn3000.hmm")
+    write_hmm(path, 3000, 3)
+    h, o = msv.Profile_HMM(path), OracleProfile(path)
+    assert h.model_length == o.model_length == 3001
+    for got, want in zip((h.match_emissions, h.insert_emissions, h.transitions), o.arrays()):
+        assert np.array_equal(bits(got), bits(want))
+    es, b, c, j = h.msv_scores()
+    assert np.array_equal(bits(es), bits(o.emission_scores()))
+    assert bits([b, c, j]).tolist() == bits(o.constants()).tolist()
+
+
 def test_sequence_transitions_match_oracle():
     import ctypes as C
     from oracle_lib import oracle
