@@ -66,7 +66,11 @@ constexpr int DPP_ROW_BCAST15 = 0x142; // row_bcast:15
 // group; -inf (the dummy M0 column, MSV_HMM.cpp:86) for the first lane of a group.
 template <int G>
 __device__ __forceinline__ float shift_in(float last, float ninf) {
-    if constexpr (G == 16) {
+    if constexpr (G < 16) {
+        static_assert(G == 4 || G == 8, "G must be 4, 8, 16, 32 or 64");
+        const float v = dpp<DPP_ROW_SHR1>(ninf, last);
+        return (threadIdx.x & (G - 1)) == 0 ? ninf : v;  // first lane of each group inside the row
+    } else if constexpr (G == 16) {
         return dpp<DPP_ROW_SHR1>(ninf, last);
     } else if constexpr (G == 32) {
         // rows 1 and 3 first receive lane 15 of rows 0 and 2; row_shr:1 then fills every lane
@@ -91,8 +95,8 @@ template <int G>
 __device__ __forceinline__ float group_max(float x) {
     x = fmaxf(x, dpp_perm<DPP_QUAD_1032>(x));
     x = fmaxf(x, dpp_perm<DPP_QUAD_2301>(x));
-    x = fmaxf(x, dpp_perm<DPP_ROW_HMIRROR>(x));
-    x = fmaxf(x, dpp_perm<DPP_ROW_MIRROR>(x));
+    if constexpr (G >= 8) x = fmaxf(x, dpp_perm<DPP_ROW_HMIRROR>(x));
+    if constexpr (G >= 16) x = fmaxf(x, dpp_perm<DPP_ROW_MIRROR>(x));
     if constexpr (G >= 32) {
         auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
         x = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
@@ -133,9 +137,9 @@ constexpr int residue_prefetch() {
     return S <= 16 ? 6 : (S <= 40 ? 3 : 1);
 }
 
-template <int S>
+template <int S, int RPF_ = residue_prefetch<S>()>
 struct Stream {
-    static constexpr int RPF = residue_prefetch<S>();
+    static constexpr int RPF = RPF_;
     float M[S];
     float J, C, N, B, loop, move;
     uint32_t pos, endpos, rows_left, seq, half;  // half: rows_left at which to fetch the next index
@@ -156,11 +160,17 @@ struct RowCtx {
 
 template <int G, int S, int WAVES, int PF, bool BIG, int D, int EXP = 0>
 __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs a) {
+    // (EXP & 64: timing-only A/B, one row of residue prefetch; 2 rows measured no faster at S=88)
+    using St = Stream<S, (EXP & 64) ? 1 : residue_prefetch<S>()>;
     static_assert(S % 4 == 0, "S must be a multiple of 4 (float4 chunks)");
     static_assert(PF >= 1 && D >= 1 && D <= 2, "PF >= 1, D in {1, 2}");
     constexpr int C4 = S / 4;
     constexpr int ROW_F4 = C4 * G;  // float4 per residue row
     constexpr int LDS_ROWS = lds_rows_for(G, S);
+    // Cross-row emission prefetch: when the ring holds a whole row (small profiles), the NEXT row's
+    // chunks are requested right after this row's last cell update, so the LDS latency hides behind
+    // the E butterfly and the specials instead of stalling the start of every row.
+    constexpr bool XROW = !BIG && D == 1 && PF >= C4 && residue_prefetch<S>() >= 2;
     static_assert(BIG == (LDS_ROWS < kTableRows), "BIG <=> table does not fit LDS");
     __shared__ float4 tab[LDS_ROWS * ROW_F4];
 
@@ -185,7 +195,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     uint32_t pending = kNone;
 
     // Start the next non-empty sequence in a stream (or retire the stream).
-    auto begin = [&](Stream<S>& st) {
+    auto begin = [&](St& st) {
         // Loop-free on purpose: a retry loop around the group broadcast here was unswitched by
         // the compiler into per-lane copies (see group_take).  An empty (or too long) record
         // instead becomes a one-row "junk" stream: its score is written now, one row is computed
@@ -228,11 +238,11 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         st.active = !retire;
         st.junk = !run;
 #pragma unroll
-        for (int q = 0; q < Stream<S>::RPF; ++q) st.r[q] = res[min(st.pos + q, st.endpos)];
+        for (int q = 0; q < St::RPF; ++q) st.r[q] = res[min(st.pos + q, st.endpos)];
     };
-    auto init = [&](Stream<S>& st) { begin(st); };
+    auto init = [&](St& st) { begin(st); };
     // Row prologue: next residue prefetch, emission row pointer, Bt, the j-1 neighbour, ring fill.
-    auto row_ptr = [&](Stream<S>& st) -> const float4* {
+    auto row_ptr = [&](St& st) -> const float4* {
         const uint32_t rr = min(st.r[0], static_cast<uint32_t>(kPoisonRow));
         if constexpr (!BIG) {
             return &tab[rr * ROW_F4 + gl];
@@ -240,9 +250,19 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             return (rr < static_cast<uint32_t>(LDS_ROWS)) ? &tab[rr * ROW_F4 + gl] : &a.etab[rr * ROW_F4 + gl];
         }
     };
-    auto prologue = [&](Stream<S>& st, auto& rc, const float4* ep) {
+    // Request the first chunks of a row (all of it when the ring holds a whole row).
+    auto fill_ring = [&](auto& rc, const float4* ep) {
         constexpr int P = std::decay_t<decltype(rc)>::kPF;
-        rc.rnext = res[min(st.pos + Stream<S>::RPF, st.endpos)];
+#pragma unroll
+        for (int q = 0; q < (P < C4 ? P : C4); ++q) rc.ring[q] = ep[(C4 - 1 - q) * G];
+    };
+    auto prologue = [&](St& st, auto& rc, const float4* ep) {
+        // (EXP & 32: timing-only, synthetic residues instead of the stream -> wrong scores)
+        if constexpr (EXP & 32) {
+            rc.rnext = (st.pos * 7u) % 20u;
+        } else {
+            rc.rnext = res[min(st.pos + St::RPF, st.endpos)];
+        }
         rc.ep = ep;
         rc.Bt = st.B + trBMk;
         rc.nbr = shift_in<G>(st.M[S - 1], NINF);
@@ -250,12 +270,11 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         rc.p1 = NINF;
         rc.p2 = NINF;
         rc.p3 = NINF;
-#pragma unroll
-        for (int q = 0; q < P; ++q) rc.ring[q] = rc.ep[(C4 - 1 - q) * G];
+        if constexpr (!XROW) fill_ring(rc, ep);
     };
     // One float4 chunk (states 4c+1 .. 4c+4 of the lane), highest state first so M[k-1] is still
     // the previous row's value; the next chunk is requested PF chunks ahead.
-    auto chunk = [&](Stream<S>& st, auto& rc, auto cc) {
+    auto chunk = [&](St& st, auto& rc, auto cc) {
         constexpr int P = std::decay_t<decltype(rc)>::kPF;
         constexpr int c = decltype(cc)::value;
         constexpr int slot = (C4 - 1 - c) % P;
@@ -280,7 +299,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         }
     };
     // Row epilogue: E over the group, the specials (MSV_HMM.cpp:107-110), cursor advance.
-    auto epilogue = [&](Stream<S>& st, auto& rc) {
+    auto epilogue = [&](St& st, auto& rc) {
         const float Elane = (EXP & 4) ? fmaxf(fmaxf(rc.p0, rc.p1), fmaxf(rc.p2, rc.p3)) : fmaxf(rc.p0, rc.p1);
         const float E = group_max<G>(Elane);
         st.J = fmaxf(st.J + st.loop, E + tEJ);
@@ -290,10 +309,10 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         ++st.pos;
         --st.rows_left;
 #pragma unroll
-        for (int q = 0; q + 1 < Stream<S>::RPF; ++q) st.r[q] = st.r[q + 1];
-        st.r[Stream<S>::RPF - 1] = rc.rnext;
+        for (int q = 0; q + 1 < St::RPF; ++q) st.r[q] = st.r[q + 1];
+        st.r[St::RPF - 1] = rc.rnext;
     };
-    auto finish = [&](Stream<S>& st) {
+    auto finish = [&](St& st) {
         const float sc = st.C + st.move;  // dp.back()[C] + tr_move (MSV_HMM.cpp:112)
         if (leader && !st.junk) {
             a.scores[st.seq] = sc;
@@ -305,15 +324,18 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // D independent sequences per lane group ("streams"): their rows interleave chunk by chunk,
     // so one stream's serial per-row section (E butterfly -> J/C/N/B -> Bt) overlaps the other
     // stream's cell updates inside the same wave.
-    Stream<S> s0, s1;
+    St s0, s1;
     init(s0);
     if constexpr (D == 2) init(s1);
 
     uint64_t t_start = 0;
     if (a.stamps) t_start = __builtin_amdgcn_s_memrealtime();
 
+    RowCtx<PF> xr;  // XROW: the ring persists across rows
+    if constexpr (XROW) fill_ring(xr, row_ptr(s0));
+
     // All chunks of one row, C4-1 .. 0, each step pinned so only the rings' registers are live.
-    auto row = [&](Stream<S>& st, auto& rc, const float4* ep) {
+    auto row = [&](St& st, auto& rc, const float4* ep) {
         prologue(st, rc, ep);
         [&]<int... I>(std::integer_sequence<int, I...>) {
             ((chunk(st, rc, std::integral_constant<int, C4 - 1 - I>{}),
@@ -340,6 +362,14 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
                 RowCtx<(EXP & 16) ? PF : (C4 < 10 ? C4 : 10)> c0;
                 row(s0, c0, &a.etab[rr * ROW_F4 + gl]);
             }
+        } else if constexpr (XROW) {
+            prologue(s0, xr, nullptr);
+            [&]<int... I>(std::integer_sequence<int, I...>) {
+                ((chunk(s0, xr, std::integral_constant<int, C4 - 1 - I>{})), ...);
+            }(std::make_integer_sequence<int, C4>{});
+            // s0.r[1] is the residue of the next row (discarded if this row ends the sequence)
+            fill_ring(xr, &tab[min(s0.r[1], static_cast<uint32_t>(kPoisonRow)) * ROW_F4 + gl]);
+            epilogue(s0, xr);
         } else if constexpr (D == 1) {
             RowCtx<PF> c0;
             row(s0, c0, row_ptr(s0));
@@ -360,7 +390,10 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         if constexpr (D == 2) {
             if (s1.rows_left == s1.half && pending == kNone) pending = group_take<G>(a.counter, leader, lane);
         }
-        if (s0.rows_left == 0) finish(s0);
+        if (s0.rows_left == 0) {
+            finish(s0);
+            if constexpr (XROW) fill_ring(xr, row_ptr(s0));
+        }
         if constexpr (D == 2) {
             if (s1.rows_left == 0) finish(s1);
         }
@@ -479,6 +512,9 @@ static const Variant kVariants[] = {
     MSV_EXPERIMENT(16, 88, 16, 4, 1, 6),
     MSV_EXPERIMENT(16, 88, 16, 3, 1, 4),
     MSV_EXPERIMENT(64, 40, 16, 2, 1, 8),
+    MSV_EXPERIMENT(16, 8, 4, 2, 1, 32),
+    MSV_EXPERIMENT(16, 8, 16, 2, 1, 32),
+    MSV_EXPERIMENT(16, 88, 16, 2, 1, 32),
 };
 
 const Variant* variants(int* count) {
