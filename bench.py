@@ -131,6 +131,21 @@ def pmc_traffic(config: str):
     return d.get("hbm_bytes_per_launch")
 
 
+def issue_ceiling_tcells():
+    """Measured instruction-mix ceiling of the cell update (profiles/r01_micro_cell_mix.jsonl:
+    tools/micro/cell_mix.hip, the kernel's exact per-chunk mix 4 v_max + 4 v_add + 2 v_max3 with no
+    memory and no per-row work, 4 waves/SIMD): cells/ns/SIMD x 1024 SIMDs -> T cells/s."""
+    path = os.path.join(ROOT, "profiles", "r01_micro_cell_mix.jsonl")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        for line in f:
+            d = json.loads(line)
+            if d["mix"].startswith("A_") and d["waves_per_simd"] == 4:
+                return d["cells_per_ns_per_simd"] * 1024 / 1000.0
+    return None
+
+
 def main():
     args = parse()
     import torch
@@ -232,6 +247,7 @@ def main():
         achieved = 3.0 * cells_per_launch / (kernel_ms * 1e-3) / 1e12
         alg_bytes = residues + n * (8 + 8 + 4 + 4) + 21 * info["lanes_per_group"] * info["states_per_lane"] * 4
         traffic = pmc_traffic(args.config)
+        ceiling = issue_ceiling_tcells()
         result = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -267,6 +283,13 @@ def main():
                 "traffic": traffic,
                 "note": "fp32 add/max ops: 3 per DP cell (cells = residues x LENG); peak = 256 CU x 128 "
                         "lanes/clk x 2.4 GHz non-FMA VALU; HBM is not the bound (see hbm)",
+            },
+            "issue_ceiling": None if ceiling is None else {
+                "tcells_per_s": round(ceiling, 3),
+                "achieved_tcells_per_s": round(cells_per_launch / (kernel_ms * 1e-3) / 1e12, 3),
+                "frac": round(cells_per_launch / (kernel_ms * 1e-3) / 1e12 / ceiling, 4),
+                "source": "profiles/r01_micro_cell_mix.jsonl (measured: v_max/v_max3 issue at half the "
+                          "v_add rate, so 2.5 VALU/cell cannot reach the nominal peak)",
             },
             "hbm": {
                 "algorithmic_bytes_per_launch": alg_bytes,

@@ -24,7 +24,7 @@ from ._native import MSVError, check
 
 __all__ = [
     "AMINO_ACIDS", "MSVError", "Profile_HMM", "FASTA_protein_sequences", "MSV_HMM", "pack_sequences",
-    "encode", "sequence_transitions", "device_count",
+    "encode", "sequence_transitions", "device_count", "score_grid", "score_grid_device",
 ]
 
 AMINO_ACIDS = "ACDEFGHIKLMNPQRSTVWY"  # MSV_HMM.cpp:29-31
@@ -204,3 +204,38 @@ class MSV_HMM:
 
     def __del__(self):
         self.close()
+
+
+def _handles(engines: Sequence[MSV_HMM]):
+    arr = (C.c_void_p * len(engines))(*[e._p for e in engines])
+    return arr
+
+
+def score_grid(engines: Sequence[MSV_HMM], seqs: Sequence[str] | None = None, *, codes: np.ndarray | None = None,
+               offsets: np.ndarray | None = None) -> np.ndarray:
+    """Profiles x sequences grid -> float32 [len(engines), n]: the reference's
+    benchmark loop over every profile for one FASTA set (benchmark_MSV.cpp:12-24,31-41), as one
+    host call: one upload, one longest-first order, one launch per profile forked onto the
+    profiles' own streams."""
+    if not engines:
+        raise ValueError("score_grid needs at least one profile")
+    if seqs is not None:
+        codes, offsets = pack_sequences(seqs)
+    codes = np.ascontiguousarray(codes, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = len(offsets) - 1
+    out = np.zeros((len(engines), n), np.float32)
+    st = _native.lib().msv_score_grid(_handles(engines), len(engines), codes.ctypes.data if codes.size else None,
+                                      offsets.ctypes.data, n, out.ctypes.data, None)
+    if st == _native.MSV_ERR_BAD_RESIDUE:
+        raise IndexError("residue outside the 20 amino acids")
+    check(st, "msv_score_grid")
+    return out
+
+
+def score_grid_device(engines: Sequence[MSV_HMM], residues_ptr: int, residues_len: int, offsets_ptr: int, n: int,
+                      scores_ptr: int, order_ptr: int | None = None, stream: int | None = None) -> None:
+    """Device-resident grid: scores_ptr -> float32 [len(engines)][n]; async on `stream`; errors via
+    each engine's check()."""
+    check(_native.lib().msv_score_grid_device(_handles(engines), len(engines), residues_ptr, residues_len,
+                                              offsets_ptr, n, order_ptr, scores_ptr, stream), "msv_score_grid_device")

@@ -37,6 +37,7 @@ EXPORTED = [
     "msv_profile_create", "msv_profile_create_from_hmm", "msv_profile_destroy", "msv_profile_describe",
     "msv_profile_reserve_length", "msv_score_batch", "msv_score_batch_device", "msv_profile_check",
     "msv_order_longest_first", "msv_variant_count", "msv_variant_name", "msv_profile_set_variant",
+    "msv_score_grid", "msv_score_grid_device",
 ]
 
 
@@ -122,6 +123,8 @@ def lib() -> C.CDLL:
         "msv_variant_count": (C.c_int, []),
         "msv_variant_name": (C.c_char_p, [C.c_int]),
         "msv_profile_set_variant": (C.c_int, [vp, C.c_char_p]),
+        "msv_score_grid": (C.c_int, [vp, C.c_uint32, vp, vp, u64, vp, vp]),
+        "msv_score_grid_device": (C.c_int, [vp, C.c_uint32, vp, u64, vp, u64, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

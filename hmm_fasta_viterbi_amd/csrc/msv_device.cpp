@@ -127,6 +127,7 @@ struct msv_profile {
     float* d_scores = nullptr;
     size_t d_scores_cap = 0;
     uint64_t* d_stamps = nullptr;  // diagnostic timeline buffer (tools only), or nullptr
+    hipEvent_t done = nullptr;     // grid API: joins this profile's stream back to the caller's
 };
 
 
@@ -240,6 +241,7 @@ void msv_profile_destroy(msv_profile* p) {
     (void)hipFree(p->d_res);
     (void)hipFree(p->d_off);
     (void)hipFree(p->d_scores);
+    if (p->done) (void)hipEventDestroy(p->done);
     if (p->stream) (void)hipStreamDestroy(p->stream);
     delete p;
 }
@@ -485,6 +487,103 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         s = msv_profile_check(p, st);
         if (s != MSV_OK) return s;
         first = last;
+    }
+    return MSV_OK;
+}
+
+msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* d_residues,
+                                 uint64_t residues_len, const uint64_t* d_offsets, uint64_t n,
+                                 const uint32_t* d_order, float* d_scores, void* stream) {
+    if (!profiles || n_profiles == 0) return MSV_ERR_INVALID_ARGUMENT;
+    for (uint32_t i = 0; i < n_profiles; ++i)
+        if (!profiles[i] || profiles[i]->device != profiles[0]->device) return MSV_ERR_INVALID_ARGUMENT;
+    if (n == 0) return MSV_OK;
+    if (!d_scores) return MSV_ERR_INVALID_ARGUMENT;
+    DeviceGuard g(profiles[0]->device);
+    if (!g.ok) return MSV_ERR_NO_DEVICE;
+    hipStream_t cs = stream ? static_cast<hipStream_t>(stream) : profiles[0]->stream;
+    hipEvent_t fork = nullptr;
+    MSV_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+    struct EventGuard {
+        hipEvent_t e;
+        ~EventGuard() { (void)hipEventDestroy(e); }
+    } fork_guard{fork};
+    MSV_HIP(hipEventRecord(fork, cs));
+    for (uint32_t i = 0; i < n_profiles; ++i) {
+        msv_profile* p = profiles[i];
+        if (!p->done) MSV_HIP(hipEventCreateWithFlags(&p->done, hipEventDisableTiming));
+        hipStream_t ps = p->stream == cs ? cs : p->stream;
+        if (ps != cs) MSV_HIP(hipStreamWaitEvent(ps, fork, 0));
+        const msv_status s = msv_score_batch_device(p, d_residues, residues_len, d_offsets, n, d_order,
+                                                    d_scores + static_cast<uint64_t>(i) * n, ps);
+        if (s != MSV_OK) return s;
+        if (ps != cs) {
+            MSV_HIP(hipEventRecord(p->done, ps));
+            MSV_HIP(hipStreamWaitEvent(cs, p->done, 0));
+        }
+    }
+    return MSV_OK;
+}
+
+msv_status msv_score_grid(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* residues,
+                          const uint64_t* offsets, uint64_t n, float* scores, void* stream) {
+    if (!profiles || n_profiles == 0 || (n && (!offsets || !scores))) return MSV_ERR_INVALID_ARGUMENT;
+    for (uint32_t i = 0; i < n_profiles; ++i)
+        if (!profiles[i] || profiles[i]->device != profiles[0]->device) return MSV_ERR_INVALID_ARGUMENT;
+    if (n == 0) return MSV_OK;
+    uint64_t maxL = 0;
+    for (uint64_t s = 0; s < n; ++s) {
+        if (offsets[s + 1] < offsets[s]) return MSV_ERR_INVALID_ARGUMENT;
+        maxL = std::max<uint64_t>(maxL, offsets[s + 1] - offsets[s]);
+    }
+    const uint64_t bytes = offsets[n] - offsets[0];
+    if (bytes && !residues) return MSV_ERR_INVALID_ARGUMENT;
+    constexpr uint64_t kChunkBytes = (1ull << 32) - (1ull << 20);
+    if (bytes >= kChunkBytes || n >= (1ull << 32) - (1ull << 24)) {  // huge batch: per profile, chunked
+        for (uint32_t i = 0; i < n_profiles; ++i) {
+            const msv_status s = msv_score_batch(profiles[i], residues, offsets, n, scores + i * n, stream);
+            if (s != MSV_OK) return s;
+        }
+        return MSV_OK;
+    }
+    for (uint32_t i = 0; i < n_profiles; ++i) {
+        const msv_status s = msv_profile_reserve_length(profiles[i], maxL);
+        if (s != MSV_OK) return s;
+    }
+    msv_profile* p0 = profiles[0];
+    DeviceGuard g(p0->device);
+    if (!g.ok) return MSV_ERR_NO_DEVICE;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p0->stream;
+    struct Buffers {
+        uint8_t* res = nullptr;
+        uint64_t* off = nullptr;
+        uint32_t* order = nullptr;
+        float* sc = nullptr;
+        ~Buffers() {
+            (void)hipFree(res);
+            (void)hipFree(off);
+            (void)hipFree(order);
+            (void)hipFree(sc);
+        }
+    } b;
+    const uint64_t total = static_cast<uint64_t>(n_profiles) * n;
+    MSV_HIP(hipMalloc(reinterpret_cast<void**>(&b.res), std::max<uint64_t>(bytes, 1)));
+    MSV_HIP(hipMalloc(reinterpret_cast<void**>(&b.off), (n + 1) * sizeof(uint64_t)));
+    MSV_HIP(hipMalloc(reinterpret_cast<void**>(&b.order), n * sizeof(uint32_t)));
+    MSV_HIP(hipMalloc(reinterpret_cast<void**>(&b.sc), total * sizeof(float)));
+    std::vector<uint64_t> rebased(n + 1);
+    for (uint64_t k = 0; k <= n; ++k) rebased[k] = offsets[k] - offsets[0];
+    if (bytes) MSV_HIP(hipMemcpyAsync(b.res, residues + offsets[0], bytes, hipMemcpyHostToDevice, st));
+    MSV_HIP(hipMemcpyAsync(b.off, rebased.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    msv_status s = msv_order_longest_first(p0, b.off, n, b.order, st);
+    if (s != MSV_OK) return s;
+    s = msv_score_grid_device(profiles, n_profiles, b.res, std::max<uint64_t>(bytes, 1), b.off, n, b.order, b.sc, st);
+    if (s != MSV_OK) return s;
+    MSV_HIP(hipMemcpyAsync(scores, b.sc, total * sizeof(float), hipMemcpyDeviceToHost, st));
+    MSV_HIP(hipStreamSynchronize(st));  // pageable host buffers above
+    for (uint32_t i = 0; i < n_profiles; ++i) {
+        s = msv_profile_check(profiles[i], st);
+        if (s != MSV_OK) return s;
     }
     return MSV_OK;
 }

@@ -79,6 +79,22 @@ std::vector<Log_score> MSV_HMM::score_batch(const Packed_sequences& packed) {
     return score_batch(packed.codes.data(), packed.offsets.data(), packed.size());
 }
 
+std::vector<std::vector<Log_score>> MSV_HMM::score_grid(const std::vector<MSV_HMM*>& profiles,
+                                                        const Protein_sequences& seqs) {
+    std::vector<msv_profile*> handles;
+    for (MSV_HMM* m : profiles) handles.push_back(m->profile_);
+    const Packed_sequences packed = Packed_sequences::pack(seqs);
+    const size_t n = packed.size();
+    std::vector<Log_score> flat(handles.size() * n);
+    const msv_status s = msv_score_grid(handles.data(), static_cast<uint32_t>(handles.size()), packed.codes.data(),
+                                        packed.offsets.data(), n, flat.data(), nullptr);
+    if (s == MSV_ERR_BAD_RESIDUE) throw std::out_of_range("residue outside the 20 amino acids");
+    check(s, "msv_score_grid");
+    std::vector<std::vector<Log_score>> out(handles.size());
+    for (size_t p = 0; p < handles.size(); ++p) out[p].assign(flat.begin() + p * n, flat.begin() + (p + 1) * n);
+    return out;
+}
+
 std::vector<Log_score> MSV_HMM::score_batch(const uint8_t* codes, const uint64_t* offsets, size_t n) {
     std::vector<Log_score> out(n);
     const msv_status s = msv_score_batch(profile_, codes, offsets, n, out.data(), nullptr);

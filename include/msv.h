@@ -157,6 +157,21 @@ msv_status msv_profile_check(msv_profile* profile, void* stream);
 msv_status msv_order_longest_first(msv_profile* profile, const uint64_t* d_offsets, uint64_t n, uint32_t* d_order,
                                    void* stream);
 
+/* ---- profiles x sequences grid ---------------------------------------------
+ * Replaces the reference's benchmark loop over every profile for one FASTA set
+ * (algorithms/benchmark_MSV.cpp:12-24,31-41: one MSV_HMM per .hmm, each scoring every sequence).
+ * Every profile keeps its own compile-time kernel variant (the analog of should_specialize,
+ * MSV_HMM.cpp:322-337); the launches are forked onto the profiles' own streams so that small
+ * batches of different profiles run concurrently, and joined back into `stream`.
+ * scores: [n_profiles][n] row-major (profile-major).  All profiles must live on one device; the
+ * same profile may appear more than once (its launches then serialise).  Errors latched by the
+ * kernels are reported by msv_profile_check on each profile (the host variant does that itself). */
+msv_status msv_score_grid(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* residues,
+                          const uint64_t* offsets, uint64_t n, float* scores, void* stream);
+msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* d_residues,
+                                 uint64_t residues_len, const uint64_t* d_offsets, uint64_t n,
+                                 const uint32_t* d_order, float* d_scores, void* stream);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -95,6 +95,10 @@ class MSV_HMM {
     std::vector<Log_score> score_batch(const Packed_sequences& packed);
     std::vector<Log_score> score_batch(const uint8_t* codes, const uint64_t* offsets, size_t n);
 
+    // Profiles x sequences grid (benchmark_MSV.cpp:12-24,31-41 as one call): result[p][s].
+    static std::vector<std::vector<Log_score>> score_grid(const std::vector<MSV_HMM*>& profiles,
+                                                          const Protein_sequences& seqs);
+
     msv_profile* handle() { return profile_; }
     size_t model_length() const { return model_length_; }
     const std::vector<float>& emission_scores() const { return emission_scores_; }

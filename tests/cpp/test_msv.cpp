@@ -54,6 +54,27 @@ int main(int argc, char** argv) {
             ++checked;
         }
     }
+    // the whole grid in one call (benchmark_MSV.cpp's loop over every profile)
+    {
+        std::vector<MSV_HMM> engines;
+        engines.reserve(golden.size());
+        for (const auto& kv : golden) engines.emplace_back(Profile_HMM(root + "/data/profile_HMMs/" + kv.first));
+        std::vector<MSV_HMM*> ptrs;
+        for (auto& e : engines) ptrs.push_back(&e);
+        auto grid = MSV_HMM::score_grid(ptrs, fasta.sequences);
+        size_t p = 0;
+        for (const auto& [prof, want] : golden) {
+            for (size_t i = 0; i < want.size(); ++i) {
+                if (!same_bits(grid[p][i], want[i])) {
+                    std::printf("test_msv failed! grid %s seq %zu: golden %a, grid %a\n", prof.c_str(), i, want[i],
+                                grid[p][i]);
+                    return 1;
+                }
+                ++checked;
+            }
+            ++p;
+        }
+    }
     // error behaviour: a residue outside the 20 throws std::out_of_range like amino_acid_num.at
     auto msv = MSV_HMM(Profile_HMM(root + "/data/profile_HMMs/100.hmm"));
     bool threw = false;

@@ -232,3 +232,53 @@ def test_synthetic_4096_auto_variant(tmp_path):
     assert e.describe()["lanes_per_group"] == 64
     assert np.array_equal(bits(e.score_batch(codes=codes, offsets=offsets)),
                           bits(OracleProfile(path).score_batch(codes, offsets)))
+
+
+def test_score_grid_example_all_profiles():
+    """every profile x fasta_like_example.fsa in one grid call, bitwise equal to the
+    reference's CPU scores (the benchmark_MSV.cpp loop shape)."""
+    fa = msv.FASTA_protein_sequences(os.path.join(ROOT, "data", "FASTA_files", "fasta_like_example.fsa"))
+    rows = read_golden_tsv("example_scores.tsv")
+    engines = [engine(p) for p in PROFILES]
+    grid = msv.score_grid(engines, fa.sequences)
+    assert grid.shape == (len(PROFILES), len(fa.sequences))
+    for k, prof in enumerate(PROFILES):
+        want = np.array([w for p, i, L, w in rows if p == prof], np.float32)
+        assert np.array_equal(bits(grid[k]), bits(want)), prof
+
+
+def test_score_grid_random_fasta_and_seeded():
+    fa = msv.FASTA_protein_sequences(os.path.join(ROOT, "data", "FASTA_files", "random_FASTA.fsa"))
+    rows = read_golden_tsv("random_fasta_scores.tsv")
+    engines = [engine(p) for p in PROFILES]
+    grid = msv.score_grid(engines, fa.sequences)
+    for k, prof in enumerate(PROFILES):
+        want = np.array([w for p, i, L, w in rows if p == prof], np.float32)
+        assert np.array_equal(bits(grid[k]), bits(want)), prof
+    codes, offsets = random_batch(31, 300, 0, 900)
+    sub = ["100.hmm", "1400.hmm", "2405.hmm", "100.hmm"]  # a repeated profile serialises on its stream
+    grid = msv.score_grid([engine(p) for p in sub], codes=codes, offsets=offsets)
+    for k, prof in enumerate(sub):
+        assert np.array_equal(bits(grid[k]), bits(engine(prof).score_batch(codes=codes, offsets=offsets))), prof
+
+
+def test_score_grid_device_torch_stream():
+    import torch
+    codes, offsets = random_batch(32, 2000, 1, 700)
+    sub = [engine(p) for p in ("300.hmm", "1901.hmm", "2207.hmm")]
+    for e in sub:
+        e.reserve_length(700)
+    dev = torch.device("cuda:0")
+    st = torch.cuda.Stream(dev)
+    r = torch.from_numpy(codes).to(dev)
+    o = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    out = torch.full((len(sub), len(offsets) - 1), float("nan"), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    msv.score_grid_device(sub, r.data_ptr(), r.numel(), o.data_ptr(), len(offsets) - 1, out.data_ptr(),
+                          None, st.cuda_stream)
+    st.synchronize()
+    for e in sub:
+        e.check(st.cuda_stream)
+    got = out.cpu().numpy()
+    for k, e in enumerate(sub):
+        assert np.array_equal(bits(got[k]), bits(e.score_batch(codes=codes, offsets=offsets)))
