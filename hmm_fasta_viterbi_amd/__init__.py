@@ -139,6 +139,9 @@ class MSV_HMM:
                                    self.tr_E_J, C.byref(p)), "msv_profile_create")
         self._p = p
         self.device = device
+        # STATS LOCAL MSV (Profile_HMM.cpp:83-85): parsed by the reference, used here for P-values
+        self.msv_mu = base_hmm.stats_local_msv_mu
+        self.msv_lambda = base_hmm.stats_local_msv_lambda
 
     # -- reference surface ------------------------------------------------------------------
     def run_on_sequence(self, seq: str) -> float:
@@ -183,6 +186,35 @@ class MSV_HMM:
 
     def reserve_length(self, max_length: int) -> None:
         check(_native.lib().msv_profile_reserve_length(self._p, max_length))
+
+    # -- MSV filter stage (HMMER3 formula, parity unpinned) --------------------
+    def pvalues(self, scores: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+        """P-values of MSV scores against this profile's STATS LOCAL MSV Gumbel (msv.h)."""
+        scores = np.ascontiguousarray(scores, np.float32)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        n = len(offsets) - 1
+        if scores.shape != (n,):
+            raise ValueError("scores and offsets disagree")
+        out = np.zeros(n, np.float64)
+        check(_native.lib().msv_pvalues(scores.ctypes.data, offsets.ctypes.data, n, self.msv_mu, self.msv_lambda,
+                                        out.ctypes.data), "msv_pvalues")
+        return out
+
+    def pvalues_device(self, scores_ptr: int, offsets_ptr: int, n: int, pvalues_ptr: int,
+                       stream: int | None = None) -> None:
+        """Device P-values (float64 out) for device scores/offsets, async on `stream`."""
+        check(_native.lib().msv_pvalues_device(self.device, scores_ptr, offsets_ptr, n, self.msv_mu, self.msv_lambda,
+                                               pvalues_ptr, stream), "msv_pvalues_device")
+
+    def msv_filter(self, seqs: Sequence[str] | None = None, *, codes: np.ndarray | None = None,
+                   offsets: np.ndarray | None = None, F1: float = 0.02):
+        """Scores, P-values and the pass mask of HMMER3's MSV filter threshold (P <= F1, default
+        0.02 as hmmsearch's --F1)."""
+        if seqs is not None:
+            codes, offsets = pack_sequences(seqs)
+        sc = self.score_batch(codes=codes, offsets=offsets)
+        pv = self.pvalues(sc, offsets)
+        return sc, pv, pv <= F1
 
     def set_variant(self, name: str) -> None:
         check(_native.lib().msv_profile_set_variant(self._p, name.encode()), f"set_variant({name})")

@@ -37,7 +37,7 @@ EXPORTED = [
     "msv_profile_create", "msv_profile_create_from_hmm", "msv_profile_destroy", "msv_profile_describe",
     "msv_profile_reserve_length", "msv_score_batch", "msv_score_batch_device", "msv_profile_check",
     "msv_order_longest_first", "msv_variant_count", "msv_variant_name", "msv_profile_set_variant",
-    "msv_score_grid", "msv_score_grid_device",
+    "msv_score_grid", "msv_score_grid_device", "msv_pvalues", "msv_pvalues_device",
 ]
 
 
@@ -125,6 +125,8 @@ def lib() -> C.CDLL:
         "msv_profile_set_variant": (C.c_int, [vp, C.c_char_p]),
         "msv_score_grid": (C.c_int, [vp, C.c_uint32, vp, vp, u64, vp, vp]),
         "msv_score_grid_device": (C.c_int, [vp, C.c_uint32, vp, u64, vp, u64, vp, vp, vp]),
+        "msv_pvalues": (C.c_int, [vp, vp, u64, C.c_float, C.c_float, vp]),
+        "msv_pvalues_device": (C.c_int, [C.c_int, vp, vp, u64, C.c_float, C.c_float, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -588,4 +588,36 @@ msv_status msv_score_grid(msv_profile* const* profiles, uint32_t n_profiles, con
     return MSV_OK;
 }
 
+// Host restatement of msvk::msv_pvalue_of (kept textually parallel; tests compare both).
+static double host_pvalue(float score, uint64_t L, float mu, float lambda) {
+    if (L == 0) return 1.0;  // empty sequence: score -inf, and L log(p1) would be 0 * -inf
+    const float p1 = static_cast<float>(L) / static_cast<float>(L + 1);
+    const float nullsc = static_cast<float>(static_cast<double>(L) * std::log(static_cast<double>(p1)) +
+                                            std::log(1.0 - static_cast<double>(p1)));
+    const float bits = (score - nullsc) / 0.69314718055994529f;
+    const double y = static_cast<double>(lambda) * (static_cast<double>(bits) - static_cast<double>(mu));
+    const double ey = -std::exp(-y);
+    return std::fabs(ey) < 5e-9 ? -ey : 1.0 - std::exp(ey);
+}
+
+msv_status msv_pvalues(const float* scores, const uint64_t* offsets, uint64_t n, float mu, float lambda,
+                       double* pvalues) {
+    if (n && (!scores || !offsets || !pvalues)) return MSV_ERR_INVALID_ARGUMENT;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (offsets[i + 1] < offsets[i]) return MSV_ERR_INVALID_ARGUMENT;
+        pvalues[i] = host_pvalue(scores[i], offsets[i + 1] - offsets[i], mu, lambda);
+    }
+    return MSV_OK;
+}
+
+msv_status msv_pvalues_device(int device, const float* d_scores, const uint64_t* d_offsets, uint64_t n, float mu,
+                              float lambda, double* d_pvalues, void* stream) {
+    if (n == 0) return MSV_OK;
+    if (!d_scores || !d_offsets || !d_pvalues) return MSV_ERR_INVALID_ARGUMENT;
+    DeviceGuard g(device);
+    if (!g.ok) return MSV_ERR_NO_DEVICE;
+    MSV_HIP(msvk::launch_pvalues(d_scores, d_offsets, n, mu, lambda, d_pvalues, static_cast<hipStream_t>(stream)));
+    return MSV_OK;
+}
+
 }  // extern "C"

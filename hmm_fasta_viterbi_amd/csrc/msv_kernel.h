@@ -45,6 +45,9 @@ struct Variant {
 
 const Variant* variants(int* count);
 hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, hipStream_t stream);
+hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t n, float mu, float lambda,
+                          double* pvalues, hipStream_t stream);
+
 hipError_t launch_order(const uint64_t* offsets, uint64_t n, uint32_t* scratch_hist, uint32_t nbins, uint32_t* order,
                         hipStream_t stream);
 

@@ -172,6 +172,19 @@ msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profil
                                  uint64_t residues_len, const uint64_t* d_offsets, uint64_t n,
                                  const uint32_t* d_order, float* d_scores, void* stream);
 
+/* ---- MSV filter P-values -----------------------------------------------------
+ * The reference parses STATS LOCAL MSV mu/lambda (data_readers/Profile_HMM.cpp:73-94) and never
+ * uses them; its README's intent is the HMMER3 filter pipeline.  This is HMMER3's formula for the
+ * MSV stage: null1 score nullsc = L log(p1) + log(1 - p1), p1 = L/(L+1) (float, as p7_bg_NullOne);
+ * bits = (score - nullsc) / ln 2 (float); P = Gumbel survival(bits; mu, lambda)
+ * = 1 - exp(-exp(-lambda (bits - mu))), with the small-tail branch -> exp(-lambda (bits - mu)).
+ * There is no reference implementation to pin against ("parity unpinned"); the device and host
+ * paths agree with a float64 restatement in tests/.  Empty sequences (score -inf) give P = 1. */
+msv_status msv_pvalues(const float* scores, const uint64_t* offsets, uint64_t n, float mu, float lambda,
+                       double* pvalues);
+msv_status msv_pvalues_device(int device, const float* d_scores, const uint64_t* d_offsets, uint64_t n, float mu,
+                              float lambda, double* d_pvalues, void* stream);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

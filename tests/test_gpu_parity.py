@@ -282,3 +282,22 @@ def test_score_grid_device_torch_stream():
     got = out.cpu().numpy()
     for k, e in enumerate(sub):
         assert np.array_equal(bits(got[k]), bits(e.score_batch(codes=codes, offsets=offsets)))
+
+
+def test_pvalues_device_matches_host():
+    """the device P-value kernel equals the host formula (float64 libm vs device
+    libm: 1e-13 relative), on GPU scores of a seeded batch, and msv_filter's pass mask uses it."""
+    import torch
+    e = engine("1400.hmm")
+    codes, offsets = random_batch(41, 3000, 0, 600)
+    sc, pv, passed = e.msv_filter(codes=codes, offsets=offsets)
+    assert passed.dtype == bool and np.array_equal(passed, pv <= 0.02)
+    dev = torch.device("cuda:0")
+    d_sc = torch.from_numpy(sc).to(dev)
+    d_off = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    d_pv = torch.zeros(len(sc), dtype=torch.float64, device=dev)
+    st = torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    e.pvalues_device(d_sc.data_ptr(), d_off.data_ptr(), len(sc), d_pv.data_ptr(), st.cuda_stream)
+    st.synchronize()
+    np.testing.assert_allclose(d_pv.cpu().numpy(), pv, rtol=1e-13, atol=0)

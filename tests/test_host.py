@@ -148,3 +148,42 @@ def test_cpp_parser_driver():
     exe = os.path.join(ROOT, "hmm_fasta_viterbi_amd", "lib", "test_parsers")
     r = subprocess.run([exe, ROOT], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def _pvalue_f64(score, L, mu, lam):
+    """float64 restatement of HMMER3's MSV-stage P-value with HMMER's float steps (msv.h)."""
+    if L == 0:
+        return 1.0
+    p1 = np.float32(np.float32(L) / np.float32(L + 1))
+    nullsc = np.float32(float(L) * np.log(np.float64(p1)) + np.log(1.0 - np.float64(p1)))
+    bits = np.float32(np.float32(np.float32(score) - nullsc) / np.float32(0.69314718055994529))
+    y = np.float64(lam) * (np.float64(bits) - np.float64(mu))
+    ey = -np.exp(-y)
+    return float(-ey if abs(ey) < 5e-9 else 1.0 - np.exp(ey))
+
+
+def test_msv_pvalues_host_formula():
+    """SURVEY 8(f)-4 (parity unpinned: no reference implementation): the C-ABI host P-values follow
+    the HMMER3 MSV-stage formula on golden reference scores, incl. L=0 (-inf) and the tails."""
+    import ctypes as C
+    z = np.load(os.path.join(GOLD, "seeded_1400.npz"))
+    scores, offsets = z["scores"].astype(np.float32), z["offsets"].astype(np.uint64)
+    h = msv.Profile_HMM(profile_path("1400.hmm"))
+    mu, lam = h.stats_local_msv_mu, h.stats_local_msv_lambda
+    n = len(offsets) - 1
+    out = np.zeros(n, np.float64)
+    from hmm_fasta_viterbi_amd import _native
+    assert _native.lib().msv_pvalues(scores.ctypes.data, offsets.ctypes.data, n, mu, lam, out.ctypes.data) == 0
+    want = np.array([_pvalue_f64(scores[i], int(offsets[i + 1] - offsets[i]), mu, lam) for i in range(n)])
+    np.testing.assert_allclose(out, want, rtol=1e-13, atol=0)
+    assert np.all((out >= 0) & (out <= 1))
+    lengths = np.diff(offsets)
+    assert np.all(out[lengths == 0] == 1.0)
+    # a very high score lands in the small-tail branch, a very low one gives P -> 1
+    hi = np.zeros(1, np.float64)
+    lo = np.zeros(1, np.float64)
+    off = np.array([0, 400], np.uint64)
+    _native.lib().msv_pvalues(np.array([200.0], np.float32).ctypes.data, off.ctypes.data, 1, mu, lam, hi.ctypes.data)
+    _native.lib().msv_pvalues(np.array([-200.0], np.float32).ctypes.data, off.ctypes.data, 1, mu, lam, lo.ctypes.data)
+    assert 0 < hi[0] < 1e-30 and lo[0] == 1.0
+    assert hi[0] == _pvalue_f64(200.0, 400, mu, lam)
