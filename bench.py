@@ -154,13 +154,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MSV_BENCH_BACKEND=gloo + MSV_BENCH_ONE_DEVICE=1 rehearse the multi-rank path on one GPU (all ranks
+    # on cuda:0, collectives on host tensors); the driver's N-GPU runs use the defaults (RCCL, one GPU
+    # per rank).
+    backend = os.environ.get("MSV_BENCH_BACKEND", "nccl")
+    if os.environ.get("MSV_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # where collective tensors live
 
     import hmm_fasta_viterbi_amd as msv
     from hmm_fasta_viterbi_amd.synthetic import random_batch
@@ -214,18 +222,22 @@ def main():
     engine.check(sh)
     elapsed = t1 - t0
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    residues_all = residues
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), float(t[1])
+        r = torch.tensor([residues], dtype=torch.int64, device=cdev)
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)  # ranks draw different batches (seed + rank)
+        residues_all = int(r[0])
 
     # Output collection (outside the timed region): RCCL all-gather of every rank's scores.
     gather_ms = None
     if world > 1:
         torch.cuda.synchronize(dev)
         g0 = time.perf_counter()
-        full = torch.empty(world * n, dtype=torch.float32, device=dev)
-        dist.all_gather_into_tensor(full, d_scores)
+        full = torch.empty(world * n, dtype=torch.float32, device=cdev)
+        dist.all_gather_into_tensor(full, d_scores.to(cdev))
         torch.cuda.synchronize(dev)
         gather_ms = (time.perf_counter() - g0) * 1e3
 
@@ -237,7 +249,7 @@ def main():
     host_scores = engine.score_batch(codes=codes, offsets=offsets)
     host_api_s = time.perf_counter() - t_h
     ok = ok and bool(np.array_equal(host_scores.view(np.uint32), scores.view(np.uint32)))
-    total_residues = residues * world
+    total_residues = residues_all
     value = total_residues * args.steps / elapsed / 1e6  # M residues / s, whole job
     gcups = value * 1e6 * leng / 1e9
 
