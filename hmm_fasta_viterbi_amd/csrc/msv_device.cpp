@@ -97,6 +97,10 @@ const msvk::Variant* pick_variant(uint32_t states) {
         const msvk::Variant& v = all[i];
         if (static_cast<uint32_t>(v.G * v.S) < states) continue;
         if (std::strncmp(v.name, "exp", 3) == 0) continue;  // timing-only experiments
+        // 4/8-lane groups are tuning candidates only: their per-lane rows are longer, which the issue
+        // model rewards, but small profiles are latency-bound and they measured no faster (100.hmm:
+        // g8_s16 0.162 ms, g16_s8 0.165 ms, g4_s28 0.219 ms).
+        if (v.G < 16) continue;
         if (!best || variant_cost(v) < variant_cost(*best)) best = &v;
     }
     return best;
@@ -113,7 +117,7 @@ struct msv_profile {
     float4* d_etab = nullptr;
     float2* d_lentab = nullptr;
     uint32_t lentab_n = 0;
-    uint32_t* d_words = nullptr;  // [0] dequeue counter, [2] sticky error bits
+    uint32_t* d_words = nullptr;  // [0] dequeue counter, [1] waves still running, [2] sticky error bits
     uint32_t* d_hist = nullptr;   // longest-first counting-sort scratch
     uint8_t* d_dummy = nullptr;   // a readable residue byte for batches with no residues
     hipStream_t stream = nullptr;
@@ -128,6 +132,7 @@ struct msv_profile {
     size_t d_scores_cap = 0;
     uint64_t* d_stamps = nullptr;  // diagnostic timeline buffer (tools only), or nullptr
     hipEvent_t done = nullptr;     // grid API: joins this profile's stream back to the caller's
+    bool counter_dirty = false;    // a launch failed after d_words may have been touched
 };
 
 
@@ -413,8 +418,13 @@ msv_status msv_score_batch_device(msv_profile* p, const uint8_t* d_residues, uin
 
     const uint64_t want = (n + p->groups_per_block - 1) / p->groups_per_block;
     const int blocks = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(p->blocks), want));
-    MSV_HIP(hipMemsetAsync(p->d_words, 0, sizeof(uint32_t), st));
+    // d_words[0..1] (next index, waves left) are zero between launches: zeroed at creation and
+    // put back by the last wave of every launch (msv_kernel.hip).  A failed launch may leave them
+    // dirty, so the next launch resets them explicitly.
+    if (p->counter_dirty) MSV_HIP(hipMemsetAsync(p->d_words, 0, 2 * sizeof(uint32_t), st));
+    p->counter_dirty = true;
     MSV_HIP(msvk::launch_variant(*p->v, dim3(blocks), a, st));
+    p->counter_dirty = false;
     return MSV_OK;
 }
 

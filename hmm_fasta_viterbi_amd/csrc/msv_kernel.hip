@@ -399,6 +399,16 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         }
         ++rows_done;
     }
+    // Self-resetting dequeue counter: the last wave of the grid to leave puts counter[0] (next
+    // index) and counter[1] (waves left) back to 0, so the next launch needs no memset.  Every
+    // wave's last dequeue atomic has returned before its exit increment.
+    if (lane == 0) {
+        const uint32_t total = gridDim.x * WAVES;
+        if (atomicAdd(a.counter + 1, 1u) == total - 1) {
+            atomicExch(a.counter, 0u);
+            atomicExch(a.counter + 1, 0u);
+        }
+    }
     // Diagnostic only (a.stamps == nullptr in production): per-wave start/end realtime (100 MHz),
     // rows issued, XCC id.  Never read by the kernel; used by tools/wave_timeline.py.
     if (a.stamps && lane == 0) {
@@ -558,9 +568,66 @@ hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, h
     return hipLaunchKernel(v.fn, grid, dim3(v.waves * 64), params, 0, stream);
 }
 
+// Small batches (n <= kSmallOrderPer * kOrderThreads): the whole counting sort in ONE launch and one
+// workgroup (histogram, scan and cursors in LDS, no memset), lengths held in registers between the
+// passes.  Replaces 4 dependent launches (~17 us of launch latency) by one (~5 us).
+constexpr int kSmallOrderPer = 16;
+
+__global__ __launch_bounds__(kOrderThreads) void order_small_kernel(const uint64_t* __restrict__ offsets, uint32_t n,
+                                                                    uint32_t nbins, uint32_t* __restrict__ order) {
+    extern __shared__ uint32_t lh[];  // [nbins] counts -> cursors, [kOrderThreads] scan partials
+    uint32_t* part = lh + nbins;
+    const uint32_t t = threadIdx.x;
+    for (uint32_t i = t; i < nbins; i += kOrderThreads) lh[i] = 0;
+    uint32_t bin[kSmallOrderPer];
+#pragma unroll
+    for (int k = 0; k < kSmallOrderPer; ++k) {
+        const uint32_t s = t + k * kOrderThreads;
+        bin[k] = s < n ? length_bin(offsets, s, nbins) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSmallOrderPer; ++k)
+        if (bin[k] != 0xFFFFFFFFu) atomicAdd(&lh[bin[k]], 1u);
+    __syncthreads();
+    // exclusive scan of lh[0..nbins): 4 consecutive bins per thread, Hillis-Steele over threads
+    uint32_t v[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = 4 * t + q;
+        v[q] = i < nbins ? lh[i] : 0u;
+        sum += v[q];
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < kOrderThreads; d <<= 1) {
+        const uint32_t x = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = 4 * t + q;
+        if (i < nbins) lh[i] = run;
+        run += v[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSmallOrderPer; ++k)
+        if (bin[k] != 0xFFFFFFFFu) order[atomicAdd(&lh[bin[k]], 1u)] = t + k * kOrderThreads;
+}
+
 hipError_t launch_order(const uint64_t* offsets, uint64_t n, uint32_t* scratch_hist, uint32_t nbins, uint32_t* order,
                         hipStream_t stream) {
     if (nbins > 4 * kOrderThreads) return hipErrorInvalidValue;
+    if (n <= static_cast<uint64_t>(kSmallOrderPer) * kOrderThreads) {
+        const size_t lds = (nbins + kOrderThreads) * sizeof(uint32_t);
+        hipLaunchKernelGGL(order_small_kernel, dim3(1), dim3(kOrderThreads), lds, stream, offsets,
+                           static_cast<uint32_t>(n), nbins, order);
+        return hipGetLastError();
+    }
     hipError_t e = hipMemsetAsync(scratch_hist, 0, nbins * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     const uint64_t blocks = std::min<uint64_t>(256, (n + 511) / 512);

@@ -301,3 +301,53 @@ def test_pvalues_device_matches_host():
     e.pvalues_device(d_sc.data_ptr(), d_off.data_ptr(), len(sc), d_pv.data_ptr(), st.cuda_stream)
     st.synchronize()
     np.testing.assert_allclose(d_pv.cpu().numpy(), pv, rtol=1e-13, atol=0)
+
+
+@pytest.mark.parametrize("n", [1, 1000, 16384, 16385, 200_000])
+def test_order_longest_first_sizes(n):
+    """Both order paths (one-launch small sort up to 16384, three-launch sort above) give a
+    permutation in non-increasing length order (lengths >= 4095 share the first bin)."""
+    import torch
+    e = engine("100.hmm")
+    _, offsets = random_batch(50 + n % 7, n, 0, 5000)
+    dev = torch.device("cuda:0")
+    o = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    order = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    st = torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    e.order_longest_first(o.data_ptr(), n, order.data_ptr(), st.cuda_stream)
+    st.synchronize()
+    perm = order.cpu().numpy().astype(np.int64)
+    assert np.array_equal(np.sort(perm), np.arange(n))
+    lens = np.minimum(np.diff(offsets.astype(np.int64))[perm], 4095)
+    assert np.all(lens[:-1] >= lens[1:])
+
+
+def test_back_to_back_launches_self_reset_counter():
+    """The dequeue counter is reset by the last wave of each launch (no memset between launches):
+    many launches of different sizes and grids on one stream, then a variant switch."""
+    import torch
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("700.hmm")))
+    e.reserve_length(900)
+    dev = torch.device("cuda:0")
+    st = torch.cuda.Stream(dev)
+    batches = [random_batch(60 + k, n, 0, 900) for k, n in enumerate((5, 70_000, 1, 3000, 70_000, 17))]
+    outs = []
+    for codes, offsets in batches:
+        r = torch.from_numpy(codes).to(dev)
+        o = torch.from_numpy(offsets.view(np.int64)).to(dev)
+        s = torch.empty(len(offsets) - 1, dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()
+        e.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), len(offsets) - 1, s.data_ptr(), None,
+                             st.cuda_stream)
+        outs.append((r, o, s))
+    e.check(st.cuda_stream)
+    for (codes, offsets), (_, _, s) in zip(batches, outs):
+        want = OracleProfile("700").score_batch(*subset(codes, offsets, np.arange(0, len(offsets) - 1, 97)))
+        got = s.cpu().numpy()[np.arange(0, len(offsets) - 1, 97)]
+        assert np.array_equal(bits(got), bits(want))
+    e.set_variant("msv_g16_s48_w12_p2_d1")
+    codes, offsets = batches[1]
+    got = e.score_batch(codes=codes, offsets=offsets)
+    assert np.array_equal(bits(got), bits(outs[1][2].cpu().numpy()))
+    e.close()
