@@ -24,7 +24,8 @@ from ._native import MSVError, check
 
 __all__ = [
     "AMINO_ACIDS", "MSVError", "Profile_HMM", "FASTA_protein_sequences", "MSV_HMM", "pack_sequences",
-    "encode", "sequence_transitions", "device_count", "score_grid", "score_grid_device",
+    "encode", "sequence_transitions", "device_count", "score_grid", "score_grid_device", "score_batch_multi",
+    "shard_bounds",
 ]
 
 AMINO_ACIDS = "ACDEFGHIKLMNPQRSTVWY"  # MSV_HMM.cpp:29-31
@@ -271,3 +272,32 @@ def score_grid_device(engines: Sequence[MSV_HMM], residues_ptr: int, residues_le
     each engine's check()."""
     check(_native.lib().msv_score_grid_device(_handles(engines), len(engines), residues_ptr, residues_len,
                                               offsets_ptr, n, order_ptr, scores_ptr, stream), "msv_score_grid_device")
+
+
+def shard_bounds(offsets: np.ndarray, n_shards: int) -> np.ndarray:
+    """uint64[n_shards + 1] contiguous, residue-balanced shard boundaries (msv_shard_bounds)."""
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    out = np.zeros(n_shards + 1, np.uint64)
+    check(_native.lib().msv_shard_bounds(offsets.ctypes.data, len(offsets) - 1, n_shards, out.ctypes.data),
+          "msv_shard_bounds")
+    return out
+
+
+def score_batch_multi(engines: Sequence[MSV_HMM], seqs: Sequence[str] | None = None, *,
+                      codes: np.ndarray | None = None, offsets: np.ndarray | None = None) -> np.ndarray:
+    """One batch over several devices from this one process (engines[k] = the profile on device k):
+    residue-balanced contiguous shards scored concurrently, scores in input order."""
+    if not engines:
+        raise ValueError("score_batch_multi needs at least one engine")
+    if seqs is not None:
+        codes, offsets = pack_sequences(seqs)
+    codes = np.ascontiguousarray(codes, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = len(offsets) - 1
+    out = np.zeros(n, np.float32)
+    st = _native.lib().msv_score_batch_multi(_handles(engines), len(engines), codes.ctypes.data if codes.size else None,
+                                             offsets.ctypes.data, n, out.ctypes.data)
+    if st == _native.MSV_ERR_BAD_RESIDUE:
+        raise IndexError("residue outside the 20 amino acids")
+    check(st, "msv_score_batch_multi")
+    return out

@@ -38,6 +38,7 @@ EXPORTED = [
     "msv_profile_reserve_length", "msv_score_batch", "msv_score_batch_device", "msv_profile_check",
     "msv_order_longest_first", "msv_variant_count", "msv_variant_name", "msv_profile_set_variant",
     "msv_score_grid", "msv_score_grid_device", "msv_pvalues", "msv_pvalues_device",
+    "msv_shard_bounds", "msv_score_batch_multi",
 ]
 
 
@@ -126,6 +127,8 @@ def lib() -> C.CDLL:
         "msv_score_grid": (C.c_int, [vp, C.c_uint32, vp, vp, u64, vp, vp]),
         "msv_score_grid_device": (C.c_int, [vp, C.c_uint32, vp, u64, vp, u64, vp, vp, vp]),
         "msv_pvalues": (C.c_int, [vp, vp, u64, C.c_float, C.c_float, vp]),
+        "msv_shard_bounds": (C.c_int, [vp, u64, C.c_uint32, vp]),
+        "msv_score_batch_multi": (C.c_int, [vp, C.c_uint32, vp, vp, u64, vp]),
         "msv_pvalues_device": (C.c_int, [C.c_int, vp, vp, u64, C.c_float, C.c_float, vp, vp]),
     }
     for name, (res, args) in sig.items():

@@ -14,6 +14,7 @@
 #include <limits>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "msv.h"
@@ -627,6 +628,49 @@ msv_status msv_pvalues_device(int device, const float* d_scores, const uint64_t*
     DeviceGuard g(device);
     if (!g.ok) return MSV_ERR_NO_DEVICE;
     MSV_HIP(msvk::launch_pvalues(d_scores, d_offsets, n, mu, lambda, d_pvalues, static_cast<hipStream_t>(stream)));
+    return MSV_OK;
+}
+
+msv_status msv_shard_bounds(const uint64_t* offsets, uint64_t n, uint32_t n_shards, uint64_t* bounds) {
+    if (!bounds || n_shards == 0 || (n && !offsets)) return MSV_ERR_INVALID_ARGUMENT;
+    bounds[0] = 0;
+    bounds[n_shards] = n;
+    if (n == 0) {
+        for (uint32_t k = 1; k < n_shards; ++k) bounds[k] = 0;
+        return MSV_OK;
+    }
+    const uint64_t total = offsets[n] - offsets[0];
+    for (uint32_t k = 1; k < n_shards; ++k) {
+        // first sequence whose END reaches the k-th residue quantile (np.searchsorted(offsets[1:], t, 'left'))
+        const unsigned __int128 q = static_cast<unsigned __int128>(total) * k / n_shards;
+        const uint64_t target = offsets[0] + static_cast<uint64_t>(q);
+        bounds[k] = static_cast<uint64_t>(std::lower_bound(offsets + 1, offsets + 1 + n, target) - (offsets + 1));
+    }
+    for (uint32_t k = 1; k <= n_shards; ++k) bounds[k] = std::min(n, std::max(bounds[k], bounds[k - 1]));
+    return MSV_OK;
+}
+
+msv_status msv_score_batch_multi(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* residues,
+                                 const uint64_t* offsets, uint64_t n, float* scores) {
+    if (!profiles || n_profiles == 0 || (n && (!offsets || !scores))) return MSV_ERR_INVALID_ARGUMENT;
+    for (uint32_t k = 0; k < n_profiles; ++k)
+        if (!profiles[k]) return MSV_ERR_INVALID_ARGUMENT;
+    if (n == 0) return MSV_OK;
+    std::vector<uint64_t> b(n_profiles + 1);
+    msv_status s = msv_shard_bounds(offsets, n, n_profiles, b.data());
+    if (s != MSV_OK) return s;
+    std::vector<msv_status> st(n_profiles, MSV_OK);
+    std::vector<std::thread> workers;
+    for (uint32_t k = 0; k < n_profiles; ++k) {
+        if (b[k + 1] == b[k]) continue;
+        workers.emplace_back([&, k] {
+            // offsets stay absolute: msv_score_batch rebases every chunk on its first offset
+            st[k] = msv_score_batch(profiles[k], residues, offsets + b[k], b[k + 1] - b[k], scores + b[k], nullptr);
+        });
+    }
+    for (auto& w : workers) w.join();
+    for (uint32_t k = 0; k < n_profiles; ++k)
+        if (st[k] != MSV_OK) return st[k];
     return MSV_OK;
 }
 

@@ -95,6 +95,19 @@ std::vector<std::vector<Log_score>> MSV_HMM::score_grid(const std::vector<MSV_HM
     return out;
 }
 
+std::vector<Log_score> MSV_HMM::score_batch_multi(const std::vector<MSV_HMM*>& per_device,
+                                                  const Protein_sequences& seqs) {
+    std::vector<msv_profile*> handles;
+    for (MSV_HMM* m : per_device) handles.push_back(m->profile_);
+    const Packed_sequences packed = Packed_sequences::pack(seqs);
+    std::vector<Log_score> out(packed.size());
+    const msv_status s = msv_score_batch_multi(handles.data(), static_cast<uint32_t>(handles.size()),
+                                               packed.codes.data(), packed.offsets.data(), packed.size(), out.data());
+    if (s == MSV_ERR_BAD_RESIDUE) throw std::out_of_range("residue outside the 20 amino acids");
+    check(s, "msv_score_batch_multi");
+    return out;
+}
+
 std::vector<Log_score> MSV_HMM::score_batch(const uint8_t* codes, const uint64_t* offsets, size_t n) {
     std::vector<Log_score> out(n);
     const msv_status s = msv_score_batch(profile_, codes, offsets, n, out.data(), nullptr);

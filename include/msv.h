@@ -172,6 +172,21 @@ msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profil
                                  uint64_t residues_len, const uint64_t* d_offsets, uint64_t n,
                                  const uint32_t* d_order, float* d_scores, void* stream);
 
+/* ---- several devices from one host thread (SURVEY 8(b) msv_score_batch_multi, 8(e)) ----------
+ * The reference has no multi-device path.  Sequences are independent, so a batch is cut into
+ * contiguous shards with ~equal residue counts (a prefix-sum split that keeps the output order):
+ * bounds[k] .. bounds[k+1] is shard k's sequence range (n_shards + 1 entries, bounds[0] = 0,
+ * bounds[n_shards] = n).  Host-only; the torch.distributed path (one process per GPU, RCCL
+ * gather) uses the same split (hmm_fasta_viterbi_amd/distributed.py). */
+msv_status msv_shard_bounds(const uint64_t* offsets, uint64_t n, uint32_t n_shards, uint64_t* bounds);
+
+/* profiles[k]: the same model created on device k (msv_profile_create_from_hmm(k, ...)).  Shard k
+ * of the batch is scored on profiles[k]'s device by its own host thread (upload, longest-first
+ * order, one launch, download), all shards concurrently; scores land in input order.  The same
+ * device may appear more than once (its shards then share the GPU). */
+msv_status msv_score_batch_multi(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* residues,
+                                 const uint64_t* offsets, uint64_t n, float* scores);
+
 /* ---- MSV filter P-values -----------------------------------------------------
  * The reference parses STATS LOCAL MSV mu/lambda (data_readers/Profile_HMM.cpp:73-94) and never
  * uses them; its README's intent is the HMMER3 filter pipeline.  This is HMMER3's formula for the

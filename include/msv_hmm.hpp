@@ -98,6 +98,9 @@ class MSV_HMM {
     // Profiles x sequences grid (benchmark_MSV.cpp:12-24,31-41 as one call): result[p][s].
     static std::vector<std::vector<Log_score>> score_grid(const std::vector<MSV_HMM*>& profiles,
                                                           const Protein_sequences& seqs);
+    // One batch sharded over several devices (profiles[k] = this model on device k), input order.
+    static std::vector<Log_score> score_batch_multi(const std::vector<MSV_HMM*>& per_device,
+                                                    const Protein_sequences& seqs);
 
     msv_profile* handle() { return profile_; }
     size_t model_length() const { return model_length_; }

@@ -351,3 +351,19 @@ def test_back_to_back_launches_self_reset_counter():
     got = e.score_batch(codes=codes, offsets=offsets)
     assert np.array_equal(bits(got), bits(outs[1][2].cpu().numpy()))
     e.close()
+
+
+def test_score_batch_multi_shards_match_single():
+    """msv_score_batch_multi: shards scored concurrently by one host thread per profile (here
+    several profiles on the available device(s)), bitwise equal to one launch, input order kept."""
+    prof = msv.Profile_HMM(profile_path("1400.hmm"))
+    ndev = msv.device_count()
+    engines = [msv.MSV_HMM(prof, device=k % ndev) for k in range(3)]
+    codes, offsets = random_batch(71, 20_000, 0, 800)
+    want = engine("1400.hmm").score_batch(codes=codes, offsets=offsets)
+    got = msv.score_batch_multi(engines, codes=codes, offsets=offsets)
+    assert np.array_equal(bits(got), bits(want))
+    few = msv.score_batch_multi(engines, codes=codes[:int(offsets[2])], offsets=offsets[:3])  # n < shards
+    assert np.array_equal(bits(few), bits(want[:2]))
+    for e in engines:
+        e.close()

@@ -187,3 +187,17 @@ def test_msv_pvalues_host_formula():
     _native.lib().msv_pvalues(np.array([-200.0], np.float32).ctypes.data, off.ctypes.data, 1, mu, lam, lo.ctypes.data)
     assert 0 < hi[0] < 1e-30 and lo[0] == 1.0
     assert hi[0] == _pvalue_f64(200.0, 400, mu, lam)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shard_bounds_c_abi_matches_distributed(world):
+    """msv_shard_bounds (C-ABI, used by msv_score_batch_multi) == distributed.shard_bounds (torch
+    path): contiguous, residue-balanced, covering, incl. empty sequences and n < world."""
+    from hmm_fasta_viterbi_amd.distributed import shard_bounds as py_bounds
+    from hmm_fasta_viterbi_amd.synthetic import random_batch
+    for seed, n in ((1, 0), (2, 1), (3, 5), (4, 1000)):
+        _, offsets = random_batch(seed, n, 0, 600)
+        b = msv.shard_bounds(offsets, world)
+        assert b[0] == 0 and b[-1] == n and np.all(np.diff(b.astype(np.int64)) >= 0)
+        assert [int(x) for x in b] == [py_bounds(offsets, world, 0)[0]] + [py_bounds(offsets, world, r)[1]
+                                                                          for r in range(world)]
