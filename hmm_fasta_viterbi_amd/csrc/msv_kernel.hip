@@ -108,6 +108,7 @@ __device__ __forceinline__ float group_max(float x) {
     return x;
 }
 
+
 template <int G>
 __device__ __forceinline__ uint32_t group_bcast(uint32_t v, int lane) {
     return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute((lane & ~(G - 1)) << 2, static_cast<int>(v)));
@@ -301,6 +302,8 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // Row epilogue: E over the group, the specials (MSV_HMM.cpp:107-110), cursor advance.
     auto epilogue = [&](St& st, auto& rc) {
         const float Elane = (EXP & 4) ? fmaxf(fmaxf(rc.p0, rc.p1), fmaxf(rc.p2, rc.p3)) : fmaxf(rc.p0, rc.p1);
+        // (G = 64: a row_bcast:15/31 + v_readlane reduction to an SGPR measured 13% slower on
+        // 2405.hmm than the permlane swaps -- the SGPR round trip stalls the row)
         const float E = group_max<G>(Elane);
         st.J = fmaxf(st.J + st.loop, E + tEJ);
         st.C = fmaxf(st.C + st.loop, E + tEC);
@@ -331,6 +334,9 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     uint64_t t_start = 0;
     if (a.stamps) t_start = __builtin_amdgcn_s_memrealtime();
 
+    // (Branch-layout hints -- __builtin_expect on the rare end-of-sequence / prefetch events, or on
+    // the LDS-row class for G = 64 -- measured no gain, and 15% LOSS for the latter on 2405.hmm.)
+
     RowCtx<PF> xr;  // XROW: the ring persists across rows
     if constexpr (XROW) fill_ring(xr, row_ptr(s0));
 
@@ -346,11 +352,17 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     };
 
     while (__any(D == 2 ? (s0.active || s1.active) : s0.active)) {
-        if constexpr (BIG && G == 64) {
+        if constexpr (BIG && G == 64 && (EXP & 256)) {
+            // (timing-only: vector row index, all rows from LDS, no readfirstlane -> wrong scores)
+            RowCtx<PF> c0;
+            row(s0, c0, &tab[(min(s0.r[0], static_cast<uint32_t>(kPoisonRow)) % LDS_ROWS) * ROW_F4 + gl]);
+        } else if constexpr (BIG && G == 64) {
             // One sequence per wave: the residue, hence the table row's home, is wave-uniform, so
             // the LDS rows and the L2 rows run as two separate (scalar-branched) row bodies with
             // precise waits -- no generic loads, no per-lane selects.  An L2 row requests up to 10
             // chunks up front to pay the L2 latency about once per row.
+            // (a vector compare with exec masking instead of readfirstlane measured 1.5% slower;
+            // without the class branch at all -- EXP & 256, wrong scores -- the row is 10% faster)
             const uint32_t rr =
                 __builtin_amdgcn_readfirstlane(min(s0.r[0], static_cast<uint32_t>(kPoisonRow)));
             // (EXP & 8: timing-only, every row served from LDS -> wrong scores; EXP & 16: L2 rows
@@ -386,9 +398,11 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             epilogue(s0, c0);
             epilogue(s1, c1);
         }
-        if (s0.rows_left == s0.half && pending == kNone) pending = group_take<G>(a.counter, leader, lane);
+        if (s0.rows_left == s0.half && pending == kNone)
+            pending = group_take<G>(a.counter, leader, lane);
         if constexpr (D == 2) {
-            if (s1.rows_left == s1.half && pending == kNone) pending = group_take<G>(a.counter, leader, lane);
+            if (s1.rows_left == s1.half && pending == kNone)
+                pending = group_take<G>(a.counter, leader, lane);
         }
         if (s0.rows_left == 0) {
             finish(s0);
@@ -553,6 +567,7 @@ static const Variant kVariants[] = {
     MSV_EXPERIMENT(16, 88, 16, 4, 1, 6),
     MSV_EXPERIMENT(16, 88, 16, 3, 1, 4),
     MSV_EXPERIMENT(64, 40, 16, 2, 1, 8),
+    MSV_EXPERIMENT(64, 40, 16, 2, 1, 256),
     MSV_EXPERIMENT(16, 8, 4, 2, 1, 32),
     MSV_EXPERIMENT(16, 8, 16, 2, 1, 32),
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 32),
