@@ -560,7 +560,9 @@ hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t
 
 static const Variant kVariants[] = {
 #include "msv_variants.inc"
-    // timing-only experiments (wrong scores by construction; selected only by name in tools/)
+#ifdef MSV_WITH_EXPERIMENTS
+    // timing-only experiments (wrong scores by construction; selected only by name in tools/;
+    // build with `make EXPERIMENTS=1`)
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 1),
     MSV_EXPERIMENT(16, 88, 16, 4, 1, 2),
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 4),
@@ -571,6 +573,7 @@ static const Variant kVariants[] = {
     MSV_EXPERIMENT(16, 8, 4, 2, 1, 32),
     MSV_EXPERIMENT(16, 8, 16, 2, 1, 32),
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 32),
+#endif
 };
 
 const Variant* variants(int* count) {
