@@ -118,12 +118,21 @@ class FASTA_protein_sequences:
             self.rejected = int(L.msv_fasta_rejected(f))
         finally:
             L.msv_fasta_destroy(f)
-        letters = np.frombuffer((AMINO_ACIDS + "#").encode(), np.uint8)
-        text = letters[np.minimum(self.codes, 20)].tobytes().decode()
-        self.sequences = ["#" + text[self.offsets[i]:self.offsets[i + 1]] for i in range(n)]
+        self._sequences = None
+
+    @property
+    def sequences(self) -> list[str]:
+        """'#'-prefixed residue strings (FASTA_protein_sequences.cpp:19-20), built on first use; the
+        packed `codes`/`offsets` are what the scorer consumes."""
+        if self._sequences is None:
+            letters = np.frombuffer((AMINO_ACIDS + "#").encode(), np.uint8)
+            text = letters[np.minimum(self.codes, 20)].tobytes().decode()
+            offs = self.offsets.tolist()
+            self._sequences = ["#" + text[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+        return self._sequences
 
     def __len__(self):
-        return len(self.sequences)
+        return len(self.offsets) - 1
 
 
 class MSV_HMM:

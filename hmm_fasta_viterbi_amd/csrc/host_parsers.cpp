@@ -6,6 +6,7 @@
 //   FASTA_protein_sequences   data_readers/FASTA_protein_sequences.cpp:9-44
 // The float rounding of every parsed value matters for bit-exact scores: probabilities are
 // expf(-1 * strtof(token)) exactly as Profile_HMM.cpp:40, with '*' parsing as 0 (p = 1).
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -16,7 +17,10 @@
 #include <sstream>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <vector>
+
+#include <sys/stat.h>
 
 #include "msv.h"
 #include "msv_hmm.hpp"
@@ -38,12 +42,18 @@ struct ResidueLut {
 const ResidueLut kLut;
 
 bool read_file(const char* path, std::string& out) {
-    std::ifstream f(path, std::ios::binary);
+    // one fstat-sized fread (the old ifstream -> ostringstream path copied the file twice)
+    std::FILE* f = std::fopen(path, "rb");
     if (!f) return false;
-    std::ostringstream ss;
-    ss << f.rdbuf();
-    out = ss.str();
-    return true;
+    struct stat st {};
+    if (fstat(fileno(f), &st) != 0 || !S_ISREG(st.st_mode)) {
+        std::fclose(f);
+        return false;
+    }
+    out.resize(static_cast<size_t>(st.st_size));
+    const size_t got = out.empty() ? 0 : std::fread(&out[0], 1, out.size(), f);
+    std::fclose(f);
+    return got == out.size();
 }
 
 // Line cursor with std::getline semantics ('\n' separated, '\r' kept).
@@ -162,52 +172,141 @@ struct FastaData {
     size_t rejected = 0;
 };
 
+// One chunk of a FASTA text: [begin, end) starts at a line start; every chunk but the first starts
+// with a '>' line, so no record spans two chunks.  codes are written into `out` (pre-sized to the
+// chunk length, an upper bound), offsets are chunk-relative record ends.
+struct FastaChunk {
+    std::vector<uint8_t> codes;
+    size_t ncodes = 0;
+    std::vector<uint64_t> ends;
+    std::vector<std::string> headers;
+    size_t rejected = 0;
+    msv_status status = MSV_OK;
+};
+
 // FASTA_protein_sequences.cpp:9-44: a '>' line opens a record, every other line is appended;
 // a record with any symbol outside {'#', 20 amino acids} is dropped (lowercase, 'X', '*', '\r',
 // ' ' all reject); empty records are kept.  A non-empty line before the first header is
 // undefined behaviour in the reference (sequences.back() on an empty vector, :22); here it is
 // MSV_ERR_PARSE, and empty lines before the first header are skipped.
-msv_status parse_fasta(const char* path, FastaData& out) {
-    std::string text;
-    if (!read_file(path, text)) return MSV_ERR_IO;
-    out.codes.reserve(text.size());
+void parse_fasta_chunk(const char* text, size_t begin, size_t end, FastaChunk& c) {
+    c.codes.resize(end - begin);
+    uint8_t* const out = c.codes.data();
+    size_t w = 0, rec_start = 0;
     bool open = false, bad = false;
-    size_t p = 0;
-    const size_t n = text.size();
-    auto close_record = [&]() {
-        if (!open) return;
-        if (bad) {
-            out.codes.resize(out.offsets.back());
-            out.headers.pop_back();
-            ++out.rejected;
-        } else {
-            out.offsets.push_back(out.codes.size());
-        }
-        open = false;
-    };
-    while (p < n) {
-        size_t e = text.find('\n', p);
-        if (e == std::string::npos) e = n;
+    size_t p = begin;
+    while (p < end) {
+        const void* nl = std::memchr(text + p, '\n', end - p);
+        const size_t e = nl ? static_cast<size_t>(static_cast<const char*>(nl) - text) : end;
         if (text[p] == '>' && e > p) {
-            close_record();
-            out.headers.emplace_back(text, p + 1, e - p - 1);
+            if (open) {
+                if (bad) {
+                    w = rec_start;
+                    c.headers.pop_back();
+                    ++c.rejected;
+                } else {
+                    c.ends.push_back(w);
+                }
+            }
+            c.headers.emplace_back(text + p + 1, e - p - 1);
             open = true;
             bad = false;
+            rec_start = w;
         } else if (!open) {
-            if (e > p) return MSV_ERR_PARSE;
+            if (e > p) {
+                c.status = MSV_ERR_PARSE;
+                return;
+            }
         } else if (!bad) {
+            // translate the whole line, then test it: no per-byte branch
+            uint8_t any_bad = 0;
             for (size_t k = p; k < e; ++k) {
-                const uint8_t c = kLut.v[static_cast<unsigned char>(text[k])];
-                if (c == 254) {
-                    bad = true;
-                    break;
-                }
-                out.codes.push_back(c);
+                const uint8_t v = kLut.v[static_cast<unsigned char>(text[k])];
+                out[w + (k - p)] = v;
+                any_bad |= static_cast<uint8_t>(v == 254);
+            }
+            if (any_bad) {
+                bad = true;
+            } else {
+                w += e - p;
             }
         }
         p = e + 1;
     }
-    close_record();
+    if (open) {
+        if (bad) {
+            w = rec_start;
+            c.headers.pop_back();
+            ++c.rejected;
+        } else {
+            c.ends.push_back(w);
+        }
+    }
+    c.ncodes = w;
+}
+
+// Whole-file read, then the text is cut into chunks at '>' line starts and parsed on up to 16 host
+// threads (~4 MiB minimum per chunk); chunk results are concatenated in order.
+msv_status parse_fasta(const char* path, FastaData& out) {
+    std::string text;
+    if (!read_file(path, text)) return MSV_ERR_IO;
+    const size_t n = text.size();
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const size_t want = std::max<size_t>(1, std::min<size_t>(hw, n / (4u << 20)));
+    std::vector<size_t> cut{0};
+    for (size_t k = 1; k < want; ++k) {
+        size_t q = std::max(cut.back() + 1, n * k / want);
+        // next line start that opens a record: "\n>"
+        while (q < n) {
+            const void* nl = std::memchr(text.data() + q, '\n', n - q);
+            if (!nl) {
+                q = n;
+                break;
+            }
+            q = static_cast<size_t>(static_cast<const char*>(nl) - text.data()) + 1;
+            if (q < n && text[q] == '>') break;
+        }
+        if (q >= n) break;
+        cut.push_back(q);
+    }
+    cut.push_back(n);
+    const size_t nchunks = cut.size() - 1;
+    std::vector<FastaChunk> chunks(nchunks);
+    {
+        std::vector<std::thread> pool;
+        for (size_t k = 1; k < nchunks; ++k)
+            pool.emplace_back([&, k] { parse_fasta_chunk(text.data(), cut[k], cut[k + 1], chunks[k]); });
+        parse_fasta_chunk(text.data(), cut[0], cut[1], chunks[0]);
+        for (auto& t : pool) t.join();
+    }
+    size_t total = 0, records = 0;
+    for (const auto& c : chunks) {
+        if (c.status != MSV_OK) return c.status;
+        total += c.ncodes;
+        records += c.ends.size();
+    }
+    out.codes.resize(total);
+    out.offsets.assign(1, 0);
+    out.offsets.reserve(records + 1);
+    out.headers.clear();
+    out.headers.reserve(records);
+    out.rejected = 0;
+    std::vector<size_t> base(nchunks, 0);
+    for (size_t k = 1; k < nchunks; ++k) base[k] = base[k - 1] + chunks[k - 1].ncodes;
+    {
+        std::vector<std::thread> pool;
+        for (size_t k = 1; k < nchunks; ++k)
+            pool.emplace_back([&, k] {
+                if (chunks[k].ncodes) std::memcpy(out.codes.data() + base[k], chunks[k].codes.data(), chunks[k].ncodes);
+            });
+        if (chunks[0].ncodes) std::memcpy(out.codes.data(), chunks[0].codes.data(), chunks[0].ncodes);
+        for (auto& t : pool) t.join();
+    }
+    for (size_t k = 0; k < nchunks; ++k) {
+        for (uint64_t e : chunks[k].ends) out.offsets.push_back(base[k] + e);
+        for (auto& h : chunks[k].headers) out.headers.push_back(std::move(h));
+        out.rejected += chunks[k].rejected;
+    }
     return MSV_OK;
 }
 

@@ -201,3 +201,71 @@ def test_shard_bounds_c_abi_matches_distributed(world):
         assert b[0] == 0 and b[-1] == n and np.all(np.diff(b.astype(np.int64)) >= 0)
         assert [int(x) for x in b] == [py_bounds(offsets, world, 0)[0]] + [py_bounds(offsets, world, r)[1]
                                                                           for r in range(world)]
+
+
+def _py_fasta(text: bytes):
+    """Line-loop restatement of FASTA_protein_sequences.cpp:9-44 (as the C++ reader documents)."""
+    lut = {c: i for i, c in enumerate(b"ACDEFGHIKLMNPQRSTVWY")}
+    lut[ord("#")] = 255
+    codes, offsets, headers, rejected = bytearray(), [0], [], 0
+    cur, bad, open_ = bytearray(), False, False
+    lines = text.split(b"\n")
+    if text.endswith(b"\n"):
+        lines = lines[:-1]
+    for line in lines:
+        if line[:1] == b">":
+            if open_:
+                if bad:
+                    rejected += 1
+                else:
+                    codes += cur
+                    offsets.append(len(codes))
+                    headers.append(hdr)
+            hdr, cur, bad, open_ = line[1:].decode("latin-1"), bytearray(), False, True
+        elif open_ and not bad:
+            for ch in line:
+                if ch not in lut:
+                    bad = True
+                    break
+                cur.append(lut[ch])
+    if open_:
+        if bad:
+            rejected += 1
+        else:
+            codes += cur
+            offsets.append(len(codes))
+            headers.append(hdr)
+    return np.frombuffer(bytes(codes), np.uint8), np.array(offsets, np.uint64), headers, rejected
+
+
+def test_fasta_reader_parallel_chunks_match_line_semantics(tmp_path):
+    """A ~20 MB file (parsed in several chunks on several threads) with rejected records (lowercase,
+    X, CR), '#' inside records, empty records and blank lines: identical to the line-loop semantics."""
+    rng = np.random.default_rng(9)
+    letters = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+    parts = []
+    for i in range(50_000):
+        L = int(rng.integers(0, 700))
+        seq = letters[rng.integers(0, 20, L)].tobytes()
+        kind = rng.integers(0, 40)
+        if kind == 0:
+            seq = seq[: L // 2] + b"x" + seq[L // 2:]
+        elif kind == 1:
+            seq = seq + b"X"
+        elif kind == 2:
+            seq = seq.replace(b"A", b"#", 1)
+        lines = [seq[k:k + 60] for k in range(0, len(seq), 60)] or [b""]
+        eol = b"\r\n" if kind == 3 else b"\n"
+        parts.append(b">rec %d desc\n" % i + eol.join(lines) + eol)
+        if kind == 4:
+            parts.append(b"\n")
+    text = b"".join(parts)
+    path = tmp_path / "big.fsa"
+    path.write_bytes(text)
+    assert len(text) > 16 << 20
+    fa = msv.FASTA_protein_sequences(str(path))
+    codes, offsets, headers, rejected = _py_fasta(text)
+    assert fa.rejected == rejected and rejected > 1000
+    assert np.array_equal(fa.offsets, offsets)
+    assert np.array_equal(fa.codes, codes)
+    assert fa.headers == headers
