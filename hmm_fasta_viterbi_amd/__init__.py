@@ -25,7 +25,7 @@ from ._native import MSVError, check
 __all__ = [
     "AMINO_ACIDS", "MSVError", "Profile_HMM", "FASTA_protein_sequences", "MSV_HMM", "pack_sequences",
     "encode", "sequence_transitions", "device_count", "score_grid", "score_grid_device", "score_batch_multi",
-    "shard_bounds",
+    "shard_bounds", "FASTA_device",
 ]
 
 AMINO_ACIDS = "ACDEFGHIKLMNPQRSTVWY"  # MSV_HMM.cpp:29-31
@@ -310,3 +310,47 @@ def score_batch_multi(engines: Sequence[MSV_HMM], seqs: Sequence[str] | None = N
         raise IndexError("residue outside the 20 amino acids")
     check(st, "msv_score_batch_multi")
     return out
+
+
+class FASTA_device:
+    """FASTA parsed on the GPU (msv_fasta_read_device / msv_fasta_parse_device): the
+    same records as FASTA_protein_sequences, left in device memory as the scorer's CSR input.
+    `codes_ptr`/`offsets_ptr` feed MSV_HMM.score_batch_device directly."""
+
+    def __init__(self, path: str | None = None, *, text_ptr: int | None = None, n: int = 0, device: int = 0,
+                 stream: int | None = None):
+        L = _native.lib()
+        f = C.c_void_p()
+        if path is not None:
+            check(L.msv_fasta_read_device(device, str(path).encode(), stream, C.byref(f)), f"FASTA_device({path})")
+        else:
+            check(L.msv_fasta_parse_device(device, text_ptr, n, stream, C.byref(f)), "msv_fasta_parse_device")
+        self._f = f
+        self.device = device
+        self.count = int(L.msv_fasta_device_count(f))
+        self.rejected = int(L.msv_fasta_device_rejected(f))
+        self.residues = int(L.msv_fasta_device_residues(f))
+        self.codes_ptr = L.msv_fasta_device_codes(f)
+        self.offsets_ptr = L.msv_fasta_device_offsets(f)
+        self.spans_ptr = L.msv_fasta_device_header_spans(f)
+
+    def download(self):
+        """(codes uint8, offsets uint64[count+1], spans uint64[count, 2]) on the host."""
+        codes = np.zeros(self.residues, np.uint8)
+        offsets = np.zeros(self.count + 1, np.uint64)
+        spans = np.zeros((self.count, 2), np.uint64)
+        check(_native.lib().msv_fasta_device_download(self._f, codes.ctypes.data if self.residues else None,
+                                                      offsets.ctypes.data, spans.ctypes.data if self.count else None),
+              "msv_fasta_device_download")
+        return codes, offsets, spans
+
+    def close(self):
+        if getattr(self, "_f", None) and _native._lib is not None:
+            _native._lib.msv_fasta_device_destroy(self._f)
+            self._f = None
+
+    def __del__(self):
+        self.close()
+
+    def __len__(self):
+        return self.count

@@ -39,6 +39,9 @@ EXPORTED = [
     "msv_order_longest_first", "msv_variant_count", "msv_variant_name", "msv_profile_set_variant",
     "msv_score_grid", "msv_score_grid_device", "msv_pvalues", "msv_pvalues_device",
     "msv_shard_bounds", "msv_score_batch_multi",
+    "msv_fasta_parse_device", "msv_fasta_read_device", "msv_fasta_device_destroy", "msv_fasta_device_count",
+    "msv_fasta_device_rejected", "msv_fasta_device_residues", "msv_fasta_device_codes", "msv_fasta_device_offsets",
+    "msv_fasta_device_header_spans", "msv_fasta_device_text", "msv_fasta_device_download",
 ]
 
 
@@ -128,6 +131,17 @@ def lib() -> C.CDLL:
         "msv_score_grid_device": (C.c_int, [vp, C.c_uint32, vp, u64, vp, u64, vp, vp, vp]),
         "msv_pvalues": (C.c_int, [vp, vp, u64, C.c_float, C.c_float, vp]),
         "msv_shard_bounds": (C.c_int, [vp, u64, C.c_uint32, vp]),
+        "msv_fasta_parse_device": (C.c_int, [C.c_int, vp, u64, vp, vp]),
+        "msv_fasta_read_device": (C.c_int, [C.c_int, C.c_char_p, vp, vp]),
+        "msv_fasta_device_destroy": (None, [vp]),
+        "msv_fasta_device_count": (u64, [vp]),
+        "msv_fasta_device_rejected": (u64, [vp]),
+        "msv_fasta_device_residues": (u64, [vp]),
+        "msv_fasta_device_codes": (vp, [vp]),
+        "msv_fasta_device_offsets": (vp, [vp]),
+        "msv_fasta_device_header_spans": (vp, [vp]),
+        "msv_fasta_device_text": (vp, [vp]),
+        "msv_fasta_device_download": (C.c_int, [vp, vp, vp, vp]),
         "msv_score_batch_multi": (C.c_int, [vp, C.c_uint32, vp, vp, u64, vp]),
         "msv_pvalues_device": (C.c_int, [C.c_int, vp, vp, u64, C.c_float, C.c_float, vp, vp]),
     }

@@ -90,6 +90,31 @@ const uint8_t* msv_fasta_codes(const msv_fasta* fasta);     /* offsets[count] by
 const uint64_t* msv_fasta_offsets(const msv_fasta* fasta);  /* count + 1 entries      */
 const char* msv_fasta_header(const msv_fasta* fasta, size_t i); /* header line without '>' */
 
+/* ---- FASTA ingest on the GPU -----------------------------------------------
+ * The same records as msv_fasta_read (bit-identical codes, offsets, header spans, rejected count),
+ * parsed by a chain of tile-scan kernels from FASTA text resident in HBM, so a batch can go from
+ * file bytes to scores without a host-side parse.  Results stay in device memory:
+ *   codes   : residues() bytes, offsets: count() + 1 uint64 (the scorer's CSR input as is),
+ *   spans   : 2 * count() uint64, (start, length) of each header inside the text (no '>').
+ * msv_fasta_parse_device takes text already in device memory (n < 2^32 - 2^16 bytes);
+ * msv_fasta_read_device reads a file through pinned 64 MiB pieces (read/copy overlapped) and keeps
+ * its own device copy of the text (msv_fasta_device_text).  Synchronous w.r.t. `stream`. */
+typedef struct msv_fasta_device msv_fasta_device;
+msv_status msv_fasta_parse_device(int device, const uint8_t* d_text, uint64_t n, void* stream,
+                                  msv_fasta_device** out);
+msv_status msv_fasta_read_device(int device, const char* path, void* stream, msv_fasta_device** out);
+void msv_fasta_device_destroy(msv_fasta_device* fasta);
+uint64_t msv_fasta_device_count(const msv_fasta_device* fasta);
+uint64_t msv_fasta_device_rejected(const msv_fasta_device* fasta);
+uint64_t msv_fasta_device_residues(const msv_fasta_device* fasta);
+const uint8_t* msv_fasta_device_codes(const msv_fasta_device* fasta);          /* device pointer */
+const uint64_t* msv_fasta_device_offsets(const msv_fasta_device* fasta);       /* device pointer */
+const uint64_t* msv_fasta_device_header_spans(const msv_fasta_device* fasta);  /* device pointer */
+const uint8_t* msv_fasta_device_text(const msv_fasta_device* fasta);  /* device copy, or NULL */
+/* Copies codes / offsets / spans to host buffers sized as above (any may be NULL). */
+msv_status msv_fasta_device_download(const msv_fasta_device* fasta, uint8_t* codes, uint64_t* offsets,
+                                     uint64_t* spans);
+
 /* Letters -> codes (A..Y -> 0..19).  Any other byte -> MSV_ERR_BAD_RESIDUE. */
 msv_status msv_encode_residues(const char* letters, size_t n, uint8_t* codes_out);
 

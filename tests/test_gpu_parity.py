@@ -424,3 +424,87 @@ def test_device_api_latches_errors_and_keeps_other_scores():
     assert np.isnan(got[50])
     assert np.array_equal(bits(got[:50]), bits(want))
     e.close()
+
+
+def _fasta_cases(tmp_path):
+    """FASTA texts for device-vs-host ingest parity: the reference's files, the golden edge cases,
+    a ~20 MB mixed file, one record on a single 300k-residue line, long headers across tiles, a
+    header at EOF without newline, blank lines before the first header, CRLF, empty file."""
+    rng = np.random.default_rng(17)
+    letters = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+    out = [os.path.join(ROOT, "data", "FASTA_files", f) for f in ("fasta_like_example.fsa", "random_FASTA.fsa")]
+    out.append(os.path.join(GOLD, "edge_cases.fsa"))
+    parts = []
+    for i in range(40_000):
+        L = int(rng.integers(0, 900))
+        seq = letters[rng.integers(0, 20, L)].tobytes()
+        kind = int(rng.integers(0, 30))
+        if kind == 0:
+            seq = seq[: L // 2] + b"z" + seq[L // 2:]
+        elif kind == 1:
+            seq = seq.replace(b"C", b"#", 1)
+        eol = b"\r\n" if kind == 2 else b"\n"
+        width = int(rng.integers(1, 120))
+        lines = [seq[k:k + width] for k in range(0, len(seq), width)] or [b""]
+        hdr = b"h%d " % i + (b"x" * int(rng.integers(0, 5000)) if kind == 3 else b"")
+        parts.append(b">" + hdr + eol + eol.join(lines) + eol + (b"\n\n" if kind == 4 else b""))
+    blobs = {
+        "mixed.fsa": b"".join(parts),
+        "oneline.fsa": b">big one\n" + letters[rng.integers(0, 20, 300_000)].tobytes() + b"\n>tail",
+        "preblank.fsa": b"\n\n\n>a\nACD\n\n>b\n\nEF\n",
+        "crlf_end.fsa": b">a\r\nACDE\r\n>b\r\nKLM",
+        "headers_only.fsa": b">a\n>b\n>c",
+        "empty.fsa": b"",
+    }
+    for name, blob in blobs.items():
+        path = tmp_path / name
+        path.write_bytes(blob)
+        out.append(str(path))
+    return out
+
+
+def test_fasta_device_matches_host_reader(tmp_path):
+    """the GPU FASTA parse (tile scans) yields exactly the host reader's records:
+    codes, offsets, rejected count and headers (from the returned spans)."""
+    for path in _fasta_cases(tmp_path):
+        host = msv.FASTA_protein_sequences(path)
+        dev = msv.FASTA_device(path)
+        codes, offsets, spans = dev.download()
+        assert dev.count == len(host.offsets) - 1 and dev.rejected == host.rejected, path
+        assert np.array_equal(offsets, host.offsets), path
+        assert np.array_equal(codes, host.codes), path
+        text = open(path, "rb").read()
+        hdrs = [text[int(a):int(a) + int(b)].decode("latin-1") for a, b in spans]
+        assert hdrs == host.headers, path
+        dev.close()
+
+
+def test_fasta_device_parse_errors_like_host(tmp_path):
+    bad = tmp_path / "bad.fsa"
+    bad.write_bytes(b"\nACDE\n>a\nAC\n")
+    from hmm_fasta_viterbi_amd._native import MSVError
+    with pytest.raises(MSVError):
+        msv.FASTA_protein_sequences(str(bad))
+    with pytest.raises(MSVError):
+        msv.FASTA_device(str(bad))
+    with pytest.raises(MSVError):
+        msv.FASTA_device(str(tmp_path / "missing.fsa"))
+
+
+def test_fasta_device_to_scores_end_to_end(tmp_path):
+    """File bytes -> GPU parse -> GPU scores, with no host parse: equal to the host path's scores."""
+    import torch
+    codes, offsets = random_batch(91, 30_000, 0, 700)
+    path = tmp_path / "batch.fsa"
+    from hmm_fasta_viterbi_amd.synthetic import write_fasta
+    write_fasta(str(path), codes, offsets)
+    e = engine("1400.hmm")
+    e.reserve_length(700)
+    dev = msv.FASTA_device(str(path))
+    s = torch.empty(dev.count, dtype=torch.float32, device="cuda:0")
+    st = torch.cuda.Stream(torch.device("cuda:0"))
+    torch.cuda.synchronize()
+    e.score_batch_device(dev.codes_ptr, dev.residues, dev.offsets_ptr, dev.count, s.data_ptr(), None, st.cuda_stream)
+    e.check(st.cuda_stream)
+    assert np.array_equal(bits(s.cpu().numpy()), bits(e.score_batch(codes=codes, offsets=offsets)))
+    dev.close()
