@@ -226,6 +226,15 @@ class MSV_HMM:
         pv = self.pvalues(sc, offsets)
         return sc, pv, pv <= F1
 
+    def score_fasta_device(self, fasta: "FASTA_device") -> np.ndarray:
+        """Scores of a GPU-parsed FASTA set (msv_score_fasta_device): no host parse, no H2D of residues."""
+        out = np.zeros(fasta.count, np.float32)
+        st = _native.lib().msv_score_fasta_device(self._p, fasta._f, out.ctypes.data)
+        if st == _native.MSV_ERR_BAD_RESIDUE:
+            raise IndexError("residue outside the 20 amino acids")
+        check(st, "msv_score_fasta_device")
+        return out
+
     def set_variant(self, name: str) -> None:
         check(_native.lib().msv_profile_set_variant(self._p, name.encode()), f"set_variant({name})")
 
@@ -330,6 +339,7 @@ class FASTA_device:
         self.count = int(L.msv_fasta_device_count(f))
         self.rejected = int(L.msv_fasta_device_rejected(f))
         self.residues = int(L.msv_fasta_device_residues(f))
+        self.max_length = int(L.msv_fasta_device_max_length(f))
         self.codes_ptr = L.msv_fasta_device_codes(f)
         self.offsets_ptr = L.msv_fasta_device_offsets(f)
         self.spans_ptr = L.msv_fasta_device_header_spans(f)

@@ -42,6 +42,7 @@ EXPORTED = [
     "msv_fasta_parse_device", "msv_fasta_read_device", "msv_fasta_device_destroy", "msv_fasta_device_count",
     "msv_fasta_device_rejected", "msv_fasta_device_residues", "msv_fasta_device_codes", "msv_fasta_device_offsets",
     "msv_fasta_device_header_spans", "msv_fasta_device_text", "msv_fasta_device_download",
+    "msv_fasta_device_max_length", "msv_score_fasta_device",
 ]
 
 
@@ -142,6 +143,8 @@ def lib() -> C.CDLL:
         "msv_fasta_device_header_spans": (vp, [vp]),
         "msv_fasta_device_text": (vp, [vp]),
         "msv_fasta_device_download": (C.c_int, [vp, vp, vp, vp]),
+        "msv_fasta_device_max_length": (u64, [vp]),
+        "msv_score_fasta_device": (C.c_int, [vp, vp, vp]),
         "msv_score_batch_multi": (C.c_int, [vp, C.c_uint32, vp, vp, u64, vp]),
         "msv_pvalues_device": (C.c_int, [C.c_int, vp, vp, u64, C.c_float, C.c_float, vp, vp]),
     }

@@ -72,7 +72,8 @@ struct Totals {
     uint32_t kept;      // records kept
     uint32_t kept_res;  // residues of kept records
     uint32_t error;     // bit0: residue bytes before the first header
-    uint32_t pad[3];
+    uint32_t max_len;   // longest kept record
+    uint32_t pad[2];
 };
 
 // Per-thread facts about its 16 bytes [i0, i0+16), independent of anything before the tile except
@@ -373,6 +374,7 @@ __global__ __launch_bounds__(kThreads) void fa_rec_write(uint32_t nrec, uint32_t
     if (r >= nrec) return;
     const uint2 e = ex[r], x = v[r];
     if (x.x) {
+        atomicMax(&tot->max_len, x.y);
         offsets[e.x] = e.y;
         const uint32_t hs = hdr_start[r];
         const uint32_t he = hdr_end[r] == kUnset ? n : hdr_end[r];  // header line ended by EOF
@@ -416,7 +418,7 @@ __global__ __launch_bounds__(kThreads) void fa_compact(const uint8_t* __restrict
 // ------------------------------------------------------------------------------------------------
 struct msv_fasta_device {
     int device = 0;
-    uint64_t count = 0, rejected = 0, residues = 0;
+    uint64_t count = 0, rejected = 0, residues = 0, max_length = 0;
     uint8_t* d_codes = nullptr;   // final residue stream (either d_stage or d_final)
     uint8_t* d_stage = nullptr;   // residues at their rank (incl. rejected records)
     uint8_t* d_final = nullptr;   // compacted stream (only when a record was rejected)
@@ -549,6 +551,7 @@ msv_status parse_on_device(msv_fasta_device* f, const uint8_t* d_text, uint64_t 
     f->count = tot.kept;
     f->rejected = nrec - tot.kept;
     f->residues = tot.kept_res;
+    f->max_length = tot.max_len;
     f->d_codes = f->d_stage;
     if (f->rejected) {
         FA_HIP(dalloc(f->d_final, tot.kept_res));
@@ -670,6 +673,7 @@ msv_status msv_fasta_device_download(const msv_fasta_device* f, uint8_t* codes, 
 uint64_t msv_fasta_device_count(const msv_fasta_device* f) { return f ? f->count : 0; }
 uint64_t msv_fasta_device_rejected(const msv_fasta_device* f) { return f ? f->rejected : 0; }
 uint64_t msv_fasta_device_residues(const msv_fasta_device* f) { return f ? f->residues : 0; }
+uint64_t msv_fasta_device_max_length(const msv_fasta_device* f) { return f ? f->max_length : 0; }
 const uint8_t* msv_fasta_device_codes(const msv_fasta_device* f) { return f ? f->d_codes : nullptr; }
 const uint64_t* msv_fasta_device_offsets(const msv_fasta_device* f) { return f ? f->d_offsets : nullptr; }
 const uint64_t* msv_fasta_device_header_spans(const msv_fasta_device* f) { return f ? f->d_spans : nullptr; }

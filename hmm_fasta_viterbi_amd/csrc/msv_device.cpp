@@ -131,6 +131,8 @@ struct msv_profile {
     size_t d_off_cap = 0;
     float* d_scores = nullptr;
     size_t d_scores_cap = 0;
+    uint32_t* d_order = nullptr;  // msv_score_fasta_device's longest-first order
+    size_t d_order_cap = 0;
     uint64_t* d_stamps = nullptr;  // diagnostic timeline buffer (tools only), or nullptr
     hipEvent_t done = nullptr;     // grid API: joins this profile's stream back to the caller's
     bool counter_dirty = false;    // a launch failed after d_words may have been touched
@@ -247,6 +249,7 @@ void msv_profile_destroy(msv_profile* p) {
     (void)hipFree(p->d_res);
     (void)hipFree(p->d_off);
     (void)hipFree(p->d_scores);
+    (void)hipFree(p->d_order);
     if (p->done) (void)hipEventDestroy(p->done);
     if (p->stream) (void)hipStreamDestroy(p->stream);
     delete p;
@@ -672,6 +675,27 @@ msv_status msv_score_batch_multi(msv_profile* const* profiles, uint32_t n_profil
     for (uint32_t k = 0; k < n_profiles; ++k)
         if (st[k] != MSV_OK) return st[k];
     return MSV_OK;
+}
+
+msv_status msv_score_fasta_device(msv_profile* p, const msv_fasta_device* fasta, float* scores) {
+    if (!p || !fasta) return MSV_ERR_INVALID_ARGUMENT;
+    const uint64_t n = msv_fasta_device_count(fasta);
+    if (n == 0) return MSV_OK;
+    if (!scores) return MSV_ERR_INVALID_ARGUMENT;
+    msv_status s = msv_profile_reserve_length(p, msv_fasta_device_max_length(fasta));
+    if (s != MSV_OK) return s;
+    DeviceGuard g(p->device);
+    if (!g.ok) return MSV_ERR_NO_DEVICE;
+    MSV_HIP(ensure(p->d_scores, p->d_scores_cap, n));
+    MSV_HIP(ensure(p->d_order, p->d_order_cap, n));
+    const uint64_t* d_off = msv_fasta_device_offsets(fasta);
+    s = msv_order_longest_first(p, d_off, n, p->d_order, p->stream);
+    if (s != MSV_OK) return s;
+    s = msv_score_batch_device(p, msv_fasta_device_codes(fasta), std::max<uint64_t>(msv_fasta_device_residues(fasta), 1),
+                               d_off, n, p->d_order, p->d_scores, p->stream);
+    if (s != MSV_OK) return s;
+    MSV_HIP(hipMemcpyAsync(scores, p->d_scores, n * sizeof(float), hipMemcpyDeviceToHost, p->stream));
+    return msv_profile_check(p, p->stream);
 }
 
 }  // extern "C"

@@ -108,6 +108,21 @@ std::vector<Log_score> MSV_HMM::score_batch_multi(const std::vector<MSV_HMM*>& p
     return out;
 }
 
+FASTA_device::FASTA_device(const std::string& file_path, int device) {
+    const msv_status s = msv_fasta_read_device(device, file_path.c_str(), nullptr, &handle_);
+    if (s != MSV_OK) throw msv_error(s, std::string(msv_status_string(s)) + ": " + file_path);
+}
+
+FASTA_device::~FASTA_device() { msv_fasta_device_destroy(handle_); }
+
+std::vector<Log_score> MSV_HMM::score_batch(const FASTA_device& fasta) {
+    std::vector<Log_score> out(fasta.size());
+    const msv_status s = msv_score_fasta_device(profile_, fasta.handle(), out.data());
+    if (s == MSV_ERR_BAD_RESIDUE) throw std::out_of_range("residue outside the 20 amino acids");
+    check(s, "msv_score_fasta_device");
+    return out;
+}
+
 std::vector<Log_score> MSV_HMM::score_batch(const uint8_t* codes, const uint64_t* offsets, size_t n) {
     std::vector<Log_score> out(n);
     const msv_status s = msv_score_batch(profile_, codes, offsets, n, out.data(), nullptr);

@@ -107,6 +107,7 @@ void msv_fasta_device_destroy(msv_fasta_device* fasta);
 uint64_t msv_fasta_device_count(const msv_fasta_device* fasta);
 uint64_t msv_fasta_device_rejected(const msv_fasta_device* fasta);
 uint64_t msv_fasta_device_residues(const msv_fasta_device* fasta);
+uint64_t msv_fasta_device_max_length(const msv_fasta_device* fasta);  /* longest record */
 const uint8_t* msv_fasta_device_codes(const msv_fasta_device* fasta);          /* device pointer */
 const uint64_t* msv_fasta_device_offsets(const msv_fasta_device* fasta);       /* device pointer */
 const uint64_t* msv_fasta_device_header_spans(const msv_fasta_device* fasta);  /* device pointer */
@@ -181,6 +182,10 @@ msv_status msv_profile_check(msv_profile* profile, void* stream);
  * (n uint32) using a counting sort on the device.  Enqueued on `stream`. */
 msv_status msv_order_longest_first(msv_profile* profile, const uint64_t* d_offsets, uint64_t n, uint32_t* d_order,
                                    void* stream);
+
+/* A GPU-parsed FASTA set (msv_fasta_read_device) scored in place: length table reserved for its
+ * longest record, longest-first order, one launch, scores copied to the host (count() floats). */
+msv_status msv_score_fasta_device(msv_profile* profile, const msv_fasta_device* fasta, float* scores);
 
 /* ---- profiles x sequences grid ---------------------------------------------
  * Replaces the reference's benchmark loop over every profile for one FASTA set

@@ -77,6 +77,21 @@ class FASTA_protein_sequences {
     size_t rejected = 0;
 };
 
+// A FASTA file parsed on the GPU (msv_fasta_read_device): the same records, left in device memory.
+class FASTA_device {
+  public:
+    explicit FASTA_device(const std::string& file_path, int device = 0);
+    ~FASTA_device();
+    FASTA_device(const FASTA_device&) = delete;
+    FASTA_device& operator=(const FASTA_device&) = delete;
+    size_t size() const { return msv_fasta_device_count(handle_); }
+    size_t rejected() const { return msv_fasta_device_rejected(handle_); }
+    const msv_fasta_device* handle() const { return handle_; }
+
+  private:
+    msv_fasta_device* handle_ = nullptr;
+};
+
 class MSV_HMM {
   public:
     explicit MSV_HMM(const Profile_HMM& base_hmm, int device = 0);
@@ -94,6 +109,7 @@ class MSV_HMM {
     std::vector<Log_score> score_batch(const Protein_sequences& seqs);
     std::vector<Log_score> score_batch(const Packed_sequences& packed);
     std::vector<Log_score> score_batch(const uint8_t* codes, const uint64_t* offsets, size_t n);
+    std::vector<Log_score> score_batch(const FASTA_device& fasta);  // GPU-parsed, scored in place
 
     // Profiles x sequences grid (benchmark_MSV.cpp:12-24,31-41 as one call): result[p][s].
     static std::vector<std::vector<Log_score>> score_grid(const std::vector<MSV_HMM*>& profiles,

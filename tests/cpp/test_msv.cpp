@@ -75,6 +75,22 @@ int main(int argc, char** argv) {
             ++p;
         }
     }
+    // the same FASTA parsed on the GPU and scored in place
+    {
+        auto gfa = FASTA_device(root + "/data/FASTA_files/fasta_like_example.fsa");
+        for (const auto& [prof, want] : golden) {
+            auto m = MSV_HMM(Profile_HMM(root + "/data/profile_HMMs/" + prof));
+            auto got = m.score_batch(gfa);
+            for (size_t i = 0; i < want.size(); ++i) {
+                if (!same_bits(got[i], want[i])) {
+                    std::printf("test_msv failed! device FASTA %s seq %zu: golden %a, got %a\n", prof.c_str(), i,
+                                want[i], got[i]);
+                    return 1;
+                }
+                ++checked;
+            }
+        }
+    }
     // error behaviour: a residue outside the 20 throws std::out_of_range like amino_acid_num.at
     auto msv = MSV_HMM(Profile_HMM(root + "/data/profile_HMMs/100.hmm"));
     bool threw = false;

@@ -508,3 +508,28 @@ def test_fasta_device_to_scores_end_to_end(tmp_path):
     e.check(st.cuda_stream)
     assert np.array_equal(bits(s.cpu().numpy()), bits(e.score_batch(codes=codes, offsets=offsets)))
     dev.close()
+
+
+def test_score_fasta_device_with_rejections_and_bad_residue(tmp_path):
+    """msv_score_fasta_device on a GPU-parsed file: rejected records dropped exactly like the host
+    reader, scores equal the host path's, a '#' inside a kept record raises like the reference."""
+    rng = np.random.default_rng(23)
+    letters = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+    parts = []
+    for i in range(5000):
+        seq = letters[rng.integers(0, 20, int(rng.integers(0, 600)))].tobytes()
+        if i % 17 == 0:
+            seq += b"b"  # rejected record
+        parts.append(b">s%d\n" % i + seq + b"\n")
+    path = tmp_path / "r.fsa"
+    path.write_bytes(b"".join(parts))
+    host = msv.FASTA_protein_sequences(str(path))
+    dev = msv.FASTA_device(str(path))
+    e = engine("700.hmm")
+    assert dev.count == len(host) and dev.rejected == host.rejected > 0
+    assert dev.max_length == int(np.diff(host.offsets.astype(np.int64)).max())
+    assert np.array_equal(bits(e.score_fasta_device(dev)), bits(e.score_batch(codes=host.codes, offsets=host.offsets)))
+    bad = tmp_path / "hash.fsa"
+    bad.write_bytes(b">a\nACD#EF\n>b\nKLM\n")
+    with pytest.raises(IndexError):
+        e.score_fasta_device(msv.FASTA_device(str(bad)))
