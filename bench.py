@@ -69,6 +69,17 @@ def cpu_threads(arg: int) -> int:
     return max(1, n)
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(profile_path, codes, offsets, gpu_scores, target_s, threads):
     """Time the reference CPU path (or the oracle port) on a bounded leading sample."""
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_msv.so")
@@ -127,6 +138,7 @@ def cpu_baseline(profile_path, codes, offsets, gpu_scores, target_s, threads):
         "seconds": sec,
         "bitwise_equal_to_gpu": match,
         "single_thread": single,
+        "cpu_model": cpu_model(),
     }
 
 
