@@ -90,6 +90,21 @@ double variant_cost(const msvk::Variant& v) {
     return (2.5 * v.S + row) * v.G * big * (v.pf == 2 ? 1.0 : 1.05) * (v.streams == 2 ? 1.15 : 1.0);
 }
 
+// Latency plan for small batches: one sequence per wave (G = 64) so a row is ~40% of the
+// instructions of a 16-lane row; the cheapest such variant covering the model (non-BIG if any).
+const msvk::Variant* pick_latency_variant(uint32_t states) {
+    int count = 0;
+    const msvk::Variant* all = msvk::variants(&count);
+    const msvk::Variant* best = nullptr;
+    for (int i = 0; i < count; ++i) {
+        const msvk::Variant& v = all[i];
+        if (v.G != 64 || static_cast<uint32_t>(v.G * v.S) < states) continue;
+        if (std::strncmp(v.name, "exp", 3) == 0) continue;
+        if (!best || variant_cost(v) < variant_cost(*best)) best = &v;
+    }
+    return best;
+}
+
 const msvk::Variant* pick_variant(uint32_t states) {
     int count = 0;
     const msvk::Variant* all = msvk::variants(&count);
@@ -109,21 +124,29 @@ const msvk::Variant* pick_variant(uint32_t states) {
 
 }  // namespace
 
+// One kernel instantiation with its emission table (in that variant's layout) and grid.
+struct Plan {
+    const msvk::Variant* v = nullptr;
+    float4* d_etab = nullptr;
+    int blocks = 0;  // persistent grid size
+    int groups_per_block = 0;
+};
+
 struct msv_profile {
     int device = 0;
     uint32_t model_length = 0;  // LENG + 1
-    const msvk::Variant* v = nullptr;
+    Plan main;                    // throughput plan (every launch unless the batch is small)
+    Plan lat;                     // latency plan for small batches (G = 64), may equal main's variant
+    bool force = false;           // msv_profile_set_variant: main plan for every batch size
+    uint64_t lat_max_n = 0;       // batches up to this many sequences take the latency plan
     float tr_B_Mk = 0, tr_E_C = 0, tr_E_J = 0;
     std::vector<float> emission_scores;  // host copy [20][model_length] (for re-layout)
-    float4* d_etab = nullptr;
     float2* d_lentab = nullptr;
     uint32_t lentab_n = 0;
     uint32_t* d_words = nullptr;  // [0] dequeue counter, [1] waves still running, [2] sticky error bits
     uint32_t* d_hist = nullptr;   // longest-first counting-sort scratch
     uint8_t* d_dummy = nullptr;   // a readable residue byte for batches with no residues
     hipStream_t stream = nullptr;
-    int blocks = 0;               // persistent grid size
-    int groups_per_block = 0;
     // host-API staging
     uint8_t* d_res = nullptr;
     size_t d_res_cap = 0;
@@ -142,7 +165,7 @@ struct msv_profile {
 // Lays the MSV table out for variant v and uploads it:
 // [row r][chunk c][lane gl] float4 = e[r][gl*S + 4c + 1 .. +4]; states beyond LENG are -inf
 // (never win a max); row 20 is the +inf poison row for codes >= 20.
-static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
+static msv_status install_plan(msv_profile* p, const msvk::Variant* v, Plan& plan) {
     const uint32_t model_length = p->model_length, R = model_length - 1;
     const int G = v->G, S = v->S, C4 = S / 4;
     std::vector<float> tab(static_cast<size_t>(msvk::kTableRows) * C4 * G * 4);
@@ -165,20 +188,40 @@ static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
         (void)hipFree(d);
         return hip_status(e);
     }
-    if (p->d_etab) {
+    if (plan.d_etab) {
         (void)hipStreamSynchronize(p->stream);
-        (void)hipFree(p->d_etab);
+        (void)hipFree(plan.d_etab);
     }
-    p->d_etab = d;
-    p->v = v;
+    plan.d_etab = d;
+    plan.v = v;
     hipDeviceProp_t prop;
     MSV_HIP(hipGetDeviceProperties(&prop, p->device));
     int per_cu = 0;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(v->fn), v->waves * 64, 0);
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
-    p->blocks = prop.multiProcessorCount * per_cu;
-    p->groups_per_block = v->waves * (64 / G) * v->streams;
+    plan.blocks = prop.multiProcessorCount * per_cu;
+    plan.groups_per_block = v->waves * (64 / G) * v->streams;
     return MSV_OK;
+}
+
+// Main plan for `v`, and the latency plan (its own table layout) unless it would be the same kernel.
+static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
+    msv_status s = install_plan(p, v, p->main);
+    if (s != MSV_OK) return s;
+    const msvk::Variant* lv = p->force ? nullptr : pick_latency_variant(p->model_length - 1);
+    // Worth it only when the 64-lane row is much shorter than the main row (per-row issue cost,
+    // as variant_cost): 1400.hmm 246 vs 96 -> 0.25 vs 0.55 ms at 512 sequences, still ahead at 8192;
+    // 100.hmm 46 vs 46 -> slower at every size (tools/tune.py, profiles/r01_latency_plan.jsonl).
+    const double main_row = 2.5 * v->S + 26.0, lat_row = lv ? 2.5 * lv->S + 36.0 : 0.0;
+    const double ratio = lv ? main_row / lat_row : 0.0;
+    if (!lv || lv == v || ratio < 1.6) {
+        if (p->lat.d_etab) (void)hipFree(p->lat.d_etab);
+        p->lat = Plan{};
+        p->lat_max_n = 0;
+        return MSV_OK;
+    }
+    p->lat_max_n = static_cast<uint64_t>(std::min(8192.0, 4096.0 * ratio / 1.6));
+    return install_plan(p, lv, p->lat);
 }
 
 extern "C" {
@@ -241,7 +284,8 @@ msv_status msv_hmm_msv_scores(const msv_hmm* hmm, float* emission_scores, float*
 void msv_profile_destroy(msv_profile* p) {
     if (!p) return;
     DeviceGuard g(p->device);
-    (void)hipFree(p->d_etab);
+    (void)hipFree(p->main.d_etab);
+    (void)hipFree(p->lat.d_etab);
     (void)hipFree(p->d_lentab);
     (void)hipFree(p->d_words);
     (void)hipFree(p->d_hist);
@@ -298,7 +342,6 @@ msv_status msv_profile_create(int device, const float* emission_scores, uint32_t
     if (!p) return MSV_ERR_OUT_OF_MEMORY;
     p->device = device;
     p->model_length = model_length;
-    p->v = v;
     p->tr_B_Mk = tr_B_Mk;
     p->tr_E_C = tr_E_C;
     p->tr_E_J = tr_E_J;
@@ -351,6 +394,7 @@ msv_status msv_profile_set_variant(msv_profile* p, const char* name) {
         if (static_cast<uint32_t>(all[i].G * all[i].S) < p->model_length - 1) return MSV_ERR_UNSUPPORTED_MODEL;
         DeviceGuard g(p->device);
         if (!g.ok) return MSV_ERR_NO_DEVICE;
+        p->force = true;  // a forced variant runs every batch (tests, tools/tune.py)
         return install_variant(p, &all[i]);
     }
     return MSV_ERR_INVALID_ARGUMENT;
@@ -365,7 +409,7 @@ msv_status msv_debug_set_stamps(msv_profile* p, uint64_t* d_stamps) {
     return MSV_OK;
 }
 
-int msv_debug_grid_waves(const msv_profile* p) { return p ? p->blocks * p->v->waves : 0; }
+int msv_debug_grid_waves(const msv_profile* p) { return p ? p->main.blocks * p->main.v->waves : 0; }
 
 msv_status msv_profile_create_from_hmm(int device, const msv_hmm* hmm, msv_profile** out) {
     if (!hmm || !out) return MSV_ERR_INVALID_ARGUMENT;
@@ -381,15 +425,16 @@ msv_status msv_profile_describe(const msv_profile* p, msv_kernel_info* out) {
     if (!p || !out) return MSV_ERR_INVALID_ARGUMENT;
     std::memset(out, 0, sizeof(*out));
     out->model_length = p->model_length;
-    out->lanes_per_group = static_cast<uint32_t>(p->v->G);
-    out->states_per_lane = static_cast<uint32_t>(p->v->S);
-    out->waves_per_block = static_cast<uint32_t>(p->v->waves);
-    out->lds_rows = static_cast<uint32_t>(p->v->lds_rows);
-    out->lds_bytes = static_cast<uint32_t>(p->v->lds_rows * p->v->G * p->v->S * 4);
-    out->blocks = static_cast<uint32_t>(p->blocks);
+    const msvk::Variant* v = p->main.v;
+    out->lanes_per_group = static_cast<uint32_t>(v->G);
+    out->states_per_lane = static_cast<uint32_t>(v->S);
+    out->waves_per_block = static_cast<uint32_t>(v->waves);
+    out->lds_rows = static_cast<uint32_t>(v->lds_rows);
+    out->lds_bytes = static_cast<uint32_t>(v->lds_rows * v->G * v->S * 4);
+    out->blocks = static_cast<uint32_t>(p->main.blocks);
     out->max_length = p->lentab_n ? p->lentab_n - 1 : 0;
     out->device = p->device;
-    std::snprintf(out->variant, sizeof(out->variant), "%s", p->v->name);
+    std::snprintf(out->variant, sizeof(out->variant), "%s", v->name);
     return MSV_OK;
 }
 
@@ -405,7 +450,10 @@ msv_status msv_score_batch_device(msv_profile* p, const uint8_t* d_residues, uin
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p->stream;
 
     msvk::KernelArgs a{};
-    a.etab = p->d_etab;
+    // Small batches take the latency plan: with fewer sequences than ~4 per SIMD the launch lasts
+    // one sequence's rows, and a 64-lane row is far shorter than a 16-lane one.
+    const Plan& plan = (p->lat.v && n <= p->lat_max_n) ? p->lat : p->main;
+    a.etab = plan.d_etab;
     a.residues = residues_len ? d_residues : p->d_dummy;
     a.offsets = d_offsets;
     a.order = d_order;
@@ -420,14 +468,14 @@ msv_status msv_score_batch_device(msv_profile* p, const uint8_t* d_residues, uin
     a.tr_E_J = p->tr_E_J;
     a.stamps = p->d_stamps;
 
-    const uint64_t want = (n + p->groups_per_block - 1) / p->groups_per_block;
-    const int blocks = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(p->blocks), want));
+    const uint64_t want = (n + plan.groups_per_block - 1) / plan.groups_per_block;
+    const int blocks = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(plan.blocks), want));
     // d_words[0..1] (next index, waves left) are zero between launches: zeroed at creation and
     // put back by the last wave of every launch (msv_kernel.hip).  A failed launch may leave them
     // dirty, so the next launch resets them explicitly.
     if (p->counter_dirty) MSV_HIP(hipMemsetAsync(p->d_words, 0, 2 * sizeof(uint32_t), st));
     p->counter_dirty = true;
-    MSV_HIP(msvk::launch_variant(*p->v, dim3(blocks), a, st));
+    MSV_HIP(msvk::launch_variant(*plan.v, dim3(blocks), a, st));
     p->counter_dirty = false;
     return MSV_OK;
 }

@@ -533,3 +533,19 @@ def test_score_fasta_device_with_rejections_and_bad_residue(tmp_path):
     bad.write_bytes(b">a\nACD#EF\n>b\nKLM\n")
     with pytest.raises(IndexError):
         e.score_fasta_device(msv.FASTA_device(str(bad)))
+
+
+@pytest.mark.parametrize("prof", ["100", "700", "1400", "1901", "2405"])
+def test_latency_plan_small_batches_match_main_plan(prof):
+    """Batches of <= 2048 sequences run the latency plan (one sequence per 64-lane wave); it must
+    give the main plan's bits (forced with set_variant) and the oracle's."""
+    codes, offsets = random_batch(101, 700, 0, 900)
+    auto = msv.MSV_HMM(msv.Profile_HMM(profile_path(prof + ".hmm")))
+    got = auto.score_batch(codes=codes, offsets=offsets)
+    forced = msv.MSV_HMM(msv.Profile_HMM(profile_path(prof + ".hmm")))
+    forced.set_variant(forced.describe()["variant"])
+    assert np.array_equal(bits(got), bits(forced.score_batch(codes=codes, offsets=offsets)))
+    sample = np.arange(0, 700, 23)
+    assert np.array_equal(bits(got[sample]), bits(OracleProfile(prof).score_batch(*subset(codes, offsets, sample))))
+    auto.close()
+    forced.close()
