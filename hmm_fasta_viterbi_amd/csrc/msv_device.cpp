@@ -39,7 +39,9 @@ struct DeviceGuard {
 
 // MSV_HMM::init_transitions_depend_on_seq (MSV_HMM.cpp:59-64) for every length < n, with the
 // host's logf (never a device logf, so the per-sequence constants are the reference's bits).
-const std::vector<float2>& host_length_table(uint32_t n) {
+// Returns a copy of the first n entries: the shared cache may grow under another thread (one host
+// thread per device in msv_score_batch_multi), so nothing refers into it outside the lock.
+std::vector<float2> host_length_table(uint32_t n) {
     static std::mutex mu;
     static std::vector<float2> table;
     std::lock_guard<std::mutex> lock(mu);
@@ -52,7 +54,7 @@ const std::vector<float2>& host_length_table(uint32_t n) {
             table[L] = make_float2(loop, move);
         }
     }
-    return table;
+    return std::vector<float2>(table.begin(), table.begin() + n);
 }
 
 template <typename T>
@@ -188,8 +190,8 @@ static msv_status install_plan(msv_profile* p, const msvk::Variant* v, Plan& pla
         (void)hipFree(d);
         return hip_status(e);
     }
-    if (plan.d_etab) {
-        (void)hipStreamSynchronize(p->stream);
+    if (plan.d_etab) {  // may be read by an in-flight launch on any stream the caller used
+        (void)hipDeviceSynchronize();
         (void)hipFree(plan.d_etab);
     }
     plan.d_etab = d;
@@ -215,7 +217,10 @@ static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
     const double main_row = 2.5 * v->S + 26.0, lat_row = lv ? 2.5 * lv->S + 36.0 : 0.0;
     const double ratio = lv ? main_row / lat_row : 0.0;
     if (!lv || lv == v || ratio < 1.6) {
-        if (p->lat.d_etab) (void)hipFree(p->lat.d_etab);
+        if (p->lat.d_etab) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(p->lat.d_etab);
+        }
         p->lat = Plan{};
         p->lat_max_n = 0;
         return MSV_OK;
@@ -307,7 +312,7 @@ msv_status msv_profile_reserve_length(msv_profile* p, uint64_t max_length) {
     DeviceGuard g(p->device);
     if (!g.ok) return MSV_ERR_NO_DEVICE;
     const uint32_t n = std::max(need, p->lentab_n * 2);
-    const std::vector<float2>& host = host_length_table(n);
+    const std::vector<float2> host = host_length_table(n);
     float2* d = nullptr;
     MSV_HIP(hipMalloc(reinterpret_cast<void**>(&d), n * sizeof(float2)));
     hipError_t e = hipMemcpy(d, host.data(), n * sizeof(float2), hipMemcpyHostToDevice);
@@ -315,9 +320,9 @@ msv_status msv_profile_reserve_length(msv_profile* p, uint64_t max_length) {
         (void)hipFree(d);
         return hip_status(e);
     }
-    // the old table may still be read by an in-flight launch on the profile's stream
+    // the old table may still be read by an in-flight launch on any stream the caller used
     if (p->d_lentab) {
-        (void)hipStreamSynchronize(p->stream);
+        (void)hipDeviceSynchronize();
         (void)hipFree(p->d_lentab);
     }
     p->d_lentab = d;

@@ -549,3 +549,20 @@ def test_latency_plan_small_batches_match_main_plan(prof):
     assert np.array_equal(bits(got[sample]), bits(OracleProfile(prof).score_batch(*subset(codes, offsets, sample))))
     auto.close()
     forced.close()
+
+
+def test_score_batch_multi_concurrent_length_table_growth():
+    """Each shard holds a sequence longer than the default length table, so every host thread of
+    msv_score_batch_multi grows its profile's table at once (shared host cache under a lock)."""
+    prof = msv.Profile_HMM(profile_path("100.hmm"))
+    ndev = msv.device_count()
+    engines = [msv.MSV_HMM(prof, device=k % ndev) for k in range(4)]
+    rng = np.random.default_rng(13)
+    lens = [140_000 + 1000 * k for k in range(4)]
+    codes = rng.integers(0, 20, sum(lens), dtype=np.uint8)
+    offsets = np.zeros(5, np.uint64)
+    offsets[1:] = np.cumsum(lens)
+    got = msv.score_batch_multi(engines, codes=codes, offsets=offsets)
+    assert np.array_equal(bits(got), bits(OracleProfile("100").score_batch(codes, offsets)))
+    for e in engines:
+        e.close()
