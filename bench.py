@@ -49,7 +49,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=12,
+                    help="untimed steps; the MI355X clock ramps over the first ~10 launches (3.8 -> 3.0 ms)")
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or 16")
