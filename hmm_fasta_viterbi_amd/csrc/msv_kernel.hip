@@ -393,7 +393,8 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             // precise waits -- no generic loads, no per-lane selects.  An L2 row requests up to 10
             // chunks up front to pay the L2 latency about once per row.
             // (a vector compare with exec masking instead of readfirstlane measured 1.5% slower;
-            // without the class branch at all -- EXP & 256, wrong scores -- the row is 10% faster)
+            // reading the class one row early into an SGPR changed nothing; without the class branch
+            // at all -- EXP & 256, wrong scores -- the row is 10% faster)
             const uint32_t rr =
                 __builtin_amdgcn_readfirstlane(min(s0.r[0], static_cast<uint32_t>(kPoisonRow)));
             // (EXP & 8: timing-only, every row served from LDS -> wrong scores; EXP & 16: L2 rows
