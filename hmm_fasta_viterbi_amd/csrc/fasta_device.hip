@@ -9,7 +9,7 @@
 //
 // Byte work, HBM-bound, no MFMA.  Every byte's role depends on the line it sits in (header or
 // not) and on how many headers / residue bytes precede it, so the parse is a set of scans over
-// 4 KiB tiles (one 256-thread block, 16 bytes per thread read as one uint4):
+// 8 KiB tiles (one 256-thread block, 32 bytes per thread read as two uint4):
 //   1. fa_tile_summary  per tile: header starts, position of its last line start, residue bytes
 //                       decidable locally, bytes of the leading partial line (whose header-ness
 //                       comes from an earlier tile);
@@ -39,8 +39,10 @@
 namespace fadev {
 
 constexpr int kThreads = 256;
-constexpr int kPerThread = 16;
-constexpr uint32_t kTile = kThreads * kPerThread;  // 4096 bytes
+constexpr int kPerThread = 16;                     // scan elements per thread
+constexpr uint32_t kTile = kThreads * kPerThread;  // scan elements per block (4096)
+constexpr int kBytesPerThread = 32;                // text bytes per thread (two uint4 loads)
+constexpr uint32_t kTileBytes = kThreads * kBytesPerThread;  // 8 KiB of text per block
 constexpr int kScanThreads = 1024;
 constexpr uint32_t kUnset = 0xFFFFFFFFu;
 constexpr uint8_t kBad = 254;
@@ -57,7 +59,9 @@ constexpr ResidueLut make_lut() {
     l.v[static_cast<unsigned char>('#')] = 255;
     return l;
 }
-__constant__ ResidueLut kLut = make_lut();
+// In global memory, not __constant__: a per-lane (divergent) index into constant memory is lowered
+// to a scalar-load waterfall loop; kernels copy this into LDS and index it there.
+__device__ const ResidueLut kLut = make_lut();
 
 struct TileCarry {
     uint32_t hdr_in;  // header-ness of the line open at the tile's first byte
@@ -76,117 +80,147 @@ struct Totals {
     uint32_t pad[2];
 };
 
-// Per-thread facts about its 16 bytes [i0, i0+16), independent of anything before the tile except
-// the previous byte (for line starts).
-struct ThreadFacts {
-    uint32_t hs, pre, res_after, last_ls;
-    bool has_ls, last_hdr;
-};
-
-__device__ __forceinline__ void load16(const uint8_t* __restrict__ T, uint32_t n, uint32_t i0, uint8_t (&b)[16]) {
-    if (i0 + 16 <= n && (reinterpret_cast<uintptr_t>(T + i0) & 15) == 0) {
-        const uint4 v = *reinterpret_cast<const uint4*>(T + i0);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+__device__ __forceinline__ void load32(const uint8_t* __restrict__ T, uint32_t n, uint32_t i0,
+                                       uint8_t (&b)[kBytesPerThread]) {
+    if (i0 + kBytesPerThread <= n && (reinterpret_cast<uintptr_t>(T + i0) & 15) == 0) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) b[k] = static_cast<uint8_t>(w[k >> 2] >> (8 * (k & 3)));
+        for (int h = 0; h < kBytesPerThread / 16; ++h) {
+            const uint4 v = *reinterpret_cast<const uint4*>(T + i0 + 16 * h);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) b[16 * h + k] = static_cast<uint8_t>(w[k >> 2] >> (8 * (k & 3)));
+        }
     } else {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) b[k] = i0 + k < n ? T[i0 + k] : static_cast<uint8_t>('\n');
+        for (int k = 0; k < kBytesPerThread; ++k) b[k] = i0 + k < n ? T[i0 + k] : static_cast<uint8_t>('\n');
     }
 }
 
-__device__ __forceinline__ ThreadFacts thread_facts(const uint8_t (&b)[16], uint8_t prev, uint32_t i0, uint32_t n) {
-    ThreadFacts f{0, 0, 0, 0, false, false};
-    bool cur_hdr = false;
-    uint8_t pv = prev;
+// A thread's 32 bytes as bit masks (bit k = byte i0 + k): branch-free per-byte work, no SGPR-mask
+// explosion from 32 unrolled data-dependent branches.
+struct ByteMasks {
+    uint32_t valid, nl, ls, hs;  // in range, '\n', line start, header start ('>' at a line start)
+};
+
+__device__ __forceinline__ ByteMasks byte_masks(const uint8_t (&b)[kBytesPerThread], uint8_t prev, uint32_t i0,
+                                                uint32_t n) {
+    ByteMasks m{0, 0, 0, 0};
+    m.valid = i0 >= n ? 0u : (n - i0 >= 32u ? 0xFFFFFFFFu : ((1u << (n - i0)) - 1u));
+    uint32_t gt = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const uint8_t c = b[k];
-        const bool valid = i0 + k < n;
-        if (valid && pv == '\n') {  // line start
-            f.has_ls = true;
-            f.last_ls = i0 + k;
-            cur_hdr = c == '>';
-            f.last_hdr = cur_hdr;
-            f.hs += cur_hdr;
-        }
-        if (valid && c != '\n') {
-            if (!f.has_ls) {
-                ++f.pre;
-            } else if (!cur_hdr) {
-                ++f.res_after;
-            }
-        }
-        pv = c;
+    for (int k = 0; k < kBytesPerThread; ++k) {
+        m.nl |= static_cast<uint32_t>(b[k] == '\n') << k;
+        gt |= static_cast<uint32_t>(b[k] == '>') << k;
+    }
+    m.nl &= m.valid;
+    m.ls = ((m.nl << 1) | static_cast<uint32_t>(prev == '\n')) & m.valid;
+    m.hs = m.ls & gt;
+    return m;
+}
+
+// Bytes whose line is a header line, given whether the line open at the thread's first byte is one.
+__device__ __forceinline__ uint32_t header_line_mask(const ByteMasks& m, bool hdr_in) {
+    uint32_t st = hdr_in ? 1u : 0u, out = 0;
+#pragma unroll
+    for (int k = 0; k < kBytesPerThread; ++k) {
+        const uint32_t ls = (m.ls >> k) & 1u;
+        st = ls ? ((m.hs >> k) & 1u) : st;
+        out |= st << k;
+    }
+    return out;
+}
+
+__device__ __forceinline__ uint32_t below(int k) { return k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1u); }
+
+struct ThreadFacts {
+    uint32_t hs, pre, res_after, last_ls;  // last_ls: tile-local position of the last line start
+    bool has_ls, last_hdr;
+};
+
+__device__ __forceinline__ ThreadFacts thread_facts(const ByteMasks& m, uint32_t i0, uint32_t t0) {
+    ThreadFacts f{};
+    const uint32_t nonnl = m.valid & ~m.nl;
+    f.has_ls = m.ls != 0;
+    const uint32_t prefix = f.has_ls ? below(__builtin_ctz(m.ls)) : 0xFFFFFFFFu;  // bytes before the first LS
+    f.pre = __builtin_popcount(nonnl & prefix);
+    f.res_after = __builtin_popcount(nonnl & ~prefix & ~header_line_mask(m, false));
+    f.hs = __builtin_popcount(m.hs);
+    if (f.has_ls) {
+        const int k = 31 - __builtin_clz(m.ls);
+        f.last_ls = i0 + k - t0;
+        f.last_hdr = (m.hs >> k) & 1u;
     }
     return f;
 }
 
-// Block-wide exclusive "last line start" scan over threads: for thread k, whether some thread < k
-// has a line start, and if so whether the last one is a header.  Hillis-Steele in LDS (8 steps).
-__device__ __forceinline__ void carry_scan(bool has_ls, bool last_hdr, bool& valid, bool& hdr) {
-    __shared__ uint32_t s[kThreads];
-    const int t = threadIdx.x;
-    uint32_t v = has_ls ? (2u | (last_hdr ? 1u : 0u)) : 0u;  // bit1 valid, bit0 hdr
-    s[t] = v;
-    __syncthreads();
-    for (int d = 1; d < kThreads; d <<= 1) {
-        const uint32_t o = t >= d ? s[t - d] : 0u;
-        __syncthreads();
-        if (!(v & 2u)) v = o;  // inclusive: keep own if valid, else take the nearest earlier valid
-        s[t] = v;
-        __syncthreads();
-    }
-    const uint32_t ex = t > 0 ? s[t - 1] : 0u;
-    __syncthreads();
-    valid = ex & 2u;
-    hdr = ex & 1u;
+// ---- wave-level DPP scans (64 lanes) and their block-level composition ---------------------------
+template <int CTRL, int ROW_MASK, bool BOUND0>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), CTRL, ROW_MASK, 0xF, BOUND0));
 }
 
-// Block-wide exclusive sum of a uint32 (Hillis-Steele), plus the block total.
-__device__ __forceinline__ uint32_t block_exclusive_sum(uint32_t x, uint32_t& total) {
-    __shared__ uint32_t s[kThreads];
-    const int t = threadIdx.x;
-    s[t] = x;
+// Inclusive scan over the wave: row_shr 1/2/4/8 inside each 16-lane row (invalid lanes read 0),
+// then row_bcast:15 / row_bcast:31 carry the row totals up.  OP 0 = add, 1 = max (identity 0).
+template <int OP>
+__device__ __forceinline__ uint32_t wave_inclusive(uint32_t x) {
+    auto f = [](uint32_t a, uint32_t b) { return OP ? max(a, b) : a + b; };
+    x = f(x, dpp_u32<0x111, 0xF, true>(x));
+    x = f(x, dpp_u32<0x112, 0xF, true>(x));
+    x = f(x, dpp_u32<0x114, 0xF, true>(x));
+    x = f(x, dpp_u32<0x118, 0xF, true>(x));
+    x = f(x, dpp_u32<0x142, 0xA, false>(x));
+    x = f(x, dpp_u32<0x143, 0xC, false>(x));
+    return x;
+}
+
+// Block-wide exclusive scan (add or max) of one uint32 per thread; `total` = block aggregate.
+// SLOT gives each scan of a kernel its own LDS exchange array (no barrier needed between them).
+template <int OP, int SLOT>
+__device__ __forceinline__ uint32_t block_exclusive_u32(uint32_t x, uint32_t& total) {
+    __shared__ uint32_t wtot[kThreads / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t inc = wave_inclusive<OP>(x);
+    // exclusive inside the wave: the previous lane's inclusive value (wave_shr:1, lane 0 reads 0)
+    const uint32_t exw =
+        static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(inc), 0x138, 0xF, 0xF, true));
+    if (lane == 63) wtot[wave] = inc;
     __syncthreads();
-    uint32_t v = x;
-    for (int d = 1; d < kThreads; d <<= 1) {
-        const uint32_t o = t >= d ? s[t - d] : 0u;
-        __syncthreads();
-        v += o;
-        s[t] = v;
-        __syncthreads();
+    uint32_t base = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) {
+        const uint32_t v = wtot[w];
+        if (w < wave) base = OP ? max(base, v) : base + v;
+        all = OP ? max(all, v) : all + v;
     }
-    total = s[kThreads - 1];
-    __syncthreads();
-    return v - x;
+    total = all;
+    return OP ? max(base, exw) : base + exw;
 }
 
 __global__ __launch_bounds__(kThreads) void fa_tile_summary(const uint8_t* __restrict__ T, uint32_t n,
                                                             uint2* __restrict__ hs_ls, uint2* __restrict__ pre_res) {
-    const uint32_t i0 = blockIdx.x * kTile + threadIdx.x * kPerThread;
-    uint8_t b[16];
-    load16(T, n, i0, b);
+    const uint32_t t0 = blockIdx.x * kTileBytes;
+    const uint32_t i0 = t0 + threadIdx.x * kBytesPerThread;
+    uint8_t b[kBytesPerThread];
+    load32(T, n, i0, b);
     const uint8_t prev = i0 == 0 ? static_cast<uint8_t>('\n') : (i0 - 1 < n ? T[i0 - 1] : static_cast<uint8_t>('\n'));
-    const ThreadFacts f = thread_facts(b, prev, i0, n);
-    bool cv, ch;
-    carry_scan(f.has_ls, f.last_hdr, cv, ch);
+    const ByteMasks bm = byte_masks(b, prev, i0, n);
+    const ThreadFacts f = thread_facts(bm, i0, t0);
+    // last line start before this thread: (tile-local position + 1) << 1 | header bit, 0 = none
+    uint32_t ls_tot;
+    const uint32_t ls = block_exclusive_u32<1, 0>(f.has_ls ? (((f.last_ls + 1) << 1) | (f.last_hdr ? 1u : 0u)) : 0u,
+                                                  ls_tot);
+    const bool cv = ls != 0, ch = ls & 1u;
     // bytes before this thread's first line start: tile prefix if no earlier thread had a line
     // start, otherwise residue iff that line is not a header
     const uint32_t pre_tile = cv ? 0u : f.pre;
     const uint32_t res = f.res_after + ((cv && !ch) ? f.pre : 0u);
-    uint32_t s_pre = 0, s_res = 0, s_hs = 0;
-    (void)block_exclusive_sum(pre_tile, s_pre);
-    (void)block_exclusive_sum(res, s_res);
-    (void)block_exclusive_sum(f.hs, s_hs);
-    __shared__ uint32_t last_ls;  // 1 + position of the tile's last line start, 0 = none
-    if (threadIdx.x == 0) last_ls = 0;
-    __syncthreads();
-    if (f.has_ls) atomicMax(&last_ls, f.last_ls + 1);
-    __syncthreads();
+    uint32_t s_hr, s_pre;
+    (void)block_exclusive_u32<0, 1>(f.hs | (res << 16), s_hr);  // both < 2^16 per tile
+    (void)block_exclusive_u32<0, 2>(pre_tile, s_pre);
     if (threadIdx.x == 0) {
-        hs_ls[blockIdx.x] = make_uint2(s_hs, last_ls);
-        pre_res[blockIdx.x] = make_uint2(s_pre, s_res);
+        const uint32_t last_ls = ls_tot ? t0 + (ls_tot >> 1) : 0u;  // 1 + absolute position, 0 = none
+        hs_ls[blockIdx.x] = make_uint2(s_hr & 0xFFFFu, last_ls);
+        pre_res[blockIdx.x] = make_uint2(s_pre, s_hr >> 16);
     }
 }
 
@@ -219,51 +253,76 @@ __global__ __launch_bounds__(kThreads) void fa_tile_emit(const uint8_t* __restri
                                                          uint8_t* __restrict__ codes, uint32_t* __restrict__ rec_start,
                                                          uint32_t* __restrict__ hdr_start, uint32_t* __restrict__ hdr_end,
                                                          uint8_t* __restrict__ bad, Totals* __restrict__ tot) {
-    const uint32_t i0 = blockIdx.x * kTile + threadIdx.x * kPerThread;
-    uint8_t b[16];
-    load16(T, n, i0, b);
+    __shared__ uint8_t stage[kTileBytes];  // this tile's residue codes, written out coalesced
+    __shared__ uint8_t lut[256];
+    lut[threadIdx.x] = kLut.v[threadIdx.x];  // kThreads == 256; the scans below barrier before use
+    const uint32_t t0 = blockIdx.x * kTileBytes;
+    const uint32_t i0 = t0 + threadIdx.x * kBytesPerThread;
+    uint8_t b[kBytesPerThread];
+    load32(T, n, i0, b);
     const uint8_t prev = i0 == 0 ? static_cast<uint8_t>('\n') : (i0 - 1 < n ? T[i0 - 1] : static_cast<uint8_t>('\n'));
-    const ThreadFacts f = thread_facts(b, prev, i0, n);
-    bool cv, ch;
-    carry_scan(f.has_ls, f.last_hdr, cv, ch);
+    const ByteMasks bm = byte_masks(b, prev, i0, n);
+    const ThreadFacts f = thread_facts(bm, i0, t0);
+    uint32_t ls_tot;
+    const uint32_t ls = block_exclusive_u32<1, 0>(f.has_ls ? (((f.last_ls + 1) << 1) | (f.last_hdr ? 1u : 0u)) : 0u,
+                                                  ls_tot);
     const TileCarry tc = carry[blockIdx.x];
-    const bool hdr_in = cv ? ch : (tc.hdr_in != 0);  // header-ness of the line open at i0
-    const uint32_t res = f.res_after + (hdr_in ? 0u : f.pre);
-    uint32_t unused;
-    uint32_t rec = tc.h_excl + block_exclusive_sum(f.hs, unused);   // header starts before i0
-    uint32_t rank = tc.r_excl + block_exclusive_sum(res, unused);   // residue bytes before i0
-    bool cur_hdr = hdr_in;
-    uint8_t pv = prev;
-    bool pre_header_bytes = false;
+    const bool hdr_in = ls ? (ls & 1u) != 0 : (tc.hdr_in != 0);  // header-ness of the line open at i0
+    const uint32_t hline = header_line_mask(bm, hdr_in);
+    const uint32_t resm = bm.valid & ~bm.nl & ~hline;  // residue bytes
+    const uint32_t res = __builtin_popcount(resm);
+    uint32_t s_hr;
+    const uint32_t ex = block_exclusive_u32<0, 1>(f.hs | (res << 16), s_hr);
+    const uint32_t rec0 = tc.h_excl + (ex & 0xFFFFu);  // header starts before i0
+    const uint32_t local0 = ex >> 16;                   // this tile's residue bytes before i0
+    // residues -> LDS stage at their tile-local rank; rejected-byte mask for the records below
+    uint32_t badm = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const uint32_t i = i0 + k;
-        const uint8_t c = b[k];
-        if (i < n) {
-            if (pv == '\n') {
-                cur_hdr = c == '>';
-                if (cur_hdr) {
-                    rec_start[rec] = rank;
-                    hdr_start[rec] = i + 1;
-                    ++rec;
-                }
-            }
-            if (c == '\n') {
-                if (cur_hdr) hdr_end[rec - 1] = i;
-            } else if (!cur_hdr) {
-                if (rec == 0) {
-                    pre_header_bytes = true;
-                } else {
-                    const uint8_t code = kLut.v[c];
-                    codes[rank] = code;
-                    if (code == kBad) bad[rec - 1] = 1;
-                }
-                ++rank;
-            }
-        }
-        pv = c;
+    for (int k = 0; k < kBytesPerThread; ++k) {
+        const uint8_t code = lut[b[k]];
+        badm |= static_cast<uint32_t>(code == kBad) << k;
+        if ((resm >> k) & 1u) stage[local0 + __builtin_popcount(resm & below(k))] = code;
+    }
+    badm &= resm;
+    // records opened here (rare): residue start and header start
+    for (uint32_t m = bm.hs; m; m &= m - 1) {
+        const int k = __builtin_ctz(m);
+        const uint32_t r = rec0 + __builtin_popcount(bm.hs & below(k));
+        rec_start[r] = tc.r_excl + local0 + __builtin_popcount(resm & below(k));
+        hdr_start[r] = i0 + k + 1;
+    }
+    // header lines ended here: the newline of a header line
+    for (uint32_t m = bm.nl & hline; m; m &= m - 1) {
+        const int k = __builtin_ctz(m);
+        hdr_end[rec0 + __builtin_popcount(bm.hs & below(k + 1)) - 1] = i0 + k;
+    }
+    // rejected records (a byte outside the alphabet) and residues before the first header
+    bool pre_header_bytes = false;
+    for (uint32_t m = badm; m; m &= m - 1) {
+        const int k = __builtin_ctz(m);
+        const uint32_t r = rec0 + __builtin_popcount(bm.hs & below(k + 1));
+        if (r) bad[r - 1] = 1;
+    }
+    if (rec0 == 0) {
+        const uint32_t before_first_hs = bm.hs ? below(__builtin_ctz(bm.hs)) : 0xFFFFFFFFu;
+        pre_header_bytes = (resm & before_first_hs) != 0;
     }
     if (pre_header_bytes) atomicOr(&tot->error, 1u);
+    __syncthreads();
+    // coalesced copy-out: bytes up to a 4-byte boundary of the output, then words, then the tail
+    const uint32_t count = s_hr >> 16;
+    uint8_t* __restrict__ out = codes + tc.r_excl;
+    const uint32_t head = min(count, (4u - (tc.r_excl & 3u)) & 3u);
+    if (threadIdx.x < head) out[threadIdx.x] = stage[threadIdx.x];
+    const uint32_t words = (count - head) >> 2;
+    uint32_t* __restrict__ outw = reinterpret_cast<uint32_t*>(out + head);
+    for (uint32_t j = threadIdx.x; j < words; j += kThreads) {
+        const uint32_t o = head + 4 * j;
+        outw[j] = static_cast<uint32_t>(stage[o]) | (static_cast<uint32_t>(stage[o + 1]) << 8) |
+                  (static_cast<uint32_t>(stage[o + 2]) << 16) | (static_cast<uint32_t>(stage[o + 3]) << 24);
+    }
+    const uint32_t tail = head + 4 * words;
+    if (tail + threadIdx.x < count) out[tail + threadIdx.x] = stage[tail + threadIdx.x];
 }
 
 // ---- hierarchical exclusive scan of uint2 elements; OPX / OPY: 0 = sum, 1 = max (identity 0) ----
@@ -374,7 +433,6 @@ __global__ __launch_bounds__(kThreads) void fa_rec_write(uint32_t nrec, uint32_t
     if (r >= nrec) return;
     const uint2 e = ex[r], x = v[r];
     if (x.x) {
-        atomicMax(&tot->max_len, x.y);
         offsets[e.x] = e.y;
         const uint32_t hs = hdr_start[r];
         const uint32_t he = hdr_end[r] == kUnset ? n : hdr_end[r];  // header line ended by EOF
@@ -387,6 +445,21 @@ __global__ __launch_bounds__(kThreads) void fa_rec_write(uint32_t nrec, uint32_t
         tot->kept = e.x + x.x;
         tot->kept_res = e.y + x.y;
     }
+}
+
+// Longest kept record from the per-block maxima of scan_reduce<1, 1> over the record values.
+__global__ __launch_bounds__(kScanThreads) void fa_max_partials(const uint2* __restrict__ part, uint32_t np,
+                                                                Totals* __restrict__ tot) {
+    __shared__ uint32_t s[kScanThreads];
+    uint32_t m = 0;
+    for (uint32_t k = threadIdx.x; k < np; k += kScanThreads) m = max(m, part[k].y);
+    s[threadIdx.x] = m;
+    __syncthreads();
+    for (uint32_t d = kScanThreads / 2; d > 0; d >>= 1) {
+        if (threadIdx.x < d) s[threadIdx.x] = max(s[threadIdx.x], s[threadIdx.x + d]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tot->max_len = s[0];
 }
 
 // Totals of the tile pass from the last tile's values.
@@ -489,7 +562,7 @@ msv_status parse_on_device(msv_fasta_device* f, const uint8_t* d_text, uint64_t 
     using namespace fadev;
     if (n >= kMaxText) return MSV_ERR_INVALID_ARGUMENT;
     const uint32_t N = static_cast<uint32_t>(n);
-    const uint32_t nt = std::max<uint32_t>(1, (N + kTile - 1) / kTile);
+    const uint32_t nt = std::max<uint32_t>(1, (N + kTileBytes - 1) / kTileBytes);
     const uint32_t tb = (nt + kThreads - 1) / kThreads;
     Scratch s;
     FA_HIP(dalloc(s.hs_ls, nt));
@@ -540,6 +613,9 @@ msv_status parse_on_device(msv_fasta_device* f, const uint8_t* d_text, uint64_t 
         const uint32_t rb = (nrec + kThreads - 1) / kThreads;
         hipLaunchKernelGGL(fa_rec_values, dim3(rb), dim3(kThreads), 0, st, nrec, s.rec_start, s.bad, s.tot, s.rv);
         FA_HIP(hipGetLastError());
+        const uint32_t npr = (nrec + kTile - 1) / kTile;
+        hipLaunchKernelGGL((scan_reduce<1, 1>), dim3(npr), dim3(kThreads), 0, st, s.rv, nrec, s.part);
+        hipLaunchKernelGGL(fa_max_partials, dim3(1), dim3(kScanThreads), 0, st, s.part, npr, s.tot);
         FA_HIP((scan_exclusive<0, 0>(s.rv, nrec, s.rv_ex, s.part, st)));
         hipLaunchKernelGGL(fa_rec_write, dim3(rb), dim3(kThreads), 0, st, nrec, N, s.rv, s.rv_ex, s.rec_start,
                            s.hdr_start, s.hdr_end, f->d_offsets, f->d_spans, s.src, s.tot);
