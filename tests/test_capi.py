@@ -66,3 +66,29 @@ def test_no_device_is_a_status_not_a_crash():
         es = np.zeros(20 * 101, np.float32)
         p = C.c_void_p()
         assert L.msv_profile_create(0, es.ctypes.data, 101, -8.5, -0.69, -0.69, C.byref(p)) == 7
+
+
+def test_host_only_entry_points_validate_arguments():
+    """Host-side C-ABI calls added after the first round of the API (grid, multi-device, P-values,
+    shard bounds, GPU FASTA) reject bad arguments with a status and never touch a device."""
+    import numpy as np
+    L = _native.lib()
+    out = np.zeros(4, np.uint64)
+    offs = np.array([0, 3, 3, 10], np.uint64)
+    assert L.msv_shard_bounds(None, 3, 2, out.ctypes.data) == 1          # offsets NULL with n > 0
+    assert L.msv_shard_bounds(offs.ctypes.data, 3, 0, out.ctypes.data) == 1  # zero shards
+    assert L.msv_shard_bounds(offs.ctypes.data, 3, 3, out.ctypes.data) == 0
+    assert list(out) == [0, 0, 2, 3]  # cut k: first sequence whose end reaches k/3 of the residues
+    assert L.msv_shard_bounds(offs.ctypes.data, 0, 3, out.ctypes.data) == 0 and list(out) == [0, 0, 0, 0]
+    pv = np.zeros(3, np.float64)
+    bad_offs = np.array([0, 5, 2, 9], np.uint64)                          # decreasing offsets
+    sc = np.zeros(3, np.float32)
+    assert L.msv_pvalues(sc.ctypes.data, bad_offs.ctypes.data, 3, -9.0, 0.7, pv.ctypes.data) == 1
+    assert L.msv_pvalues(None, None, 0, -9.0, 0.7, None) == 0             # empty batch
+    assert L.msv_score_grid(None, 0, None, None, 0, None, None) == 1
+    assert L.msv_score_batch_multi(None, 0, None, None, 0, None) == 1
+    f = C.c_void_p()
+    assert L.msv_fasta_parse_device(0, None, 10, None, C.byref(f)) == 1  # text NULL with n > 0
+    assert L.msv_fasta_read_device(0, None, None, C.byref(f)) == 1
+    assert L.msv_fasta_device_count(None) == 0 and L.msv_fasta_device_codes(None) is None
+    assert L.msv_score_fasta_device(None, None, None) == 1
