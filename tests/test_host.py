@@ -269,3 +269,22 @@ def test_fasta_reader_parallel_chunks_match_line_semantics(tmp_path):
     assert np.array_equal(fa.offsets, offsets)
     assert np.array_equal(fa.codes, codes)
     assert fa.headers == headers
+
+
+def test_native_random_fasta_generator_format(tmp_path):
+    """lib/random_fasta (seeded mt19937_64) writes the reference generator's format
+    (random_FASTA_generator.py:1-16): same line structure as data/FASTA_files/random_FASTA.fsa by
+    default, seeded and reproducible, length range honoured."""
+    exe = os.path.join(ROOT, "hmm_fasta_viterbi_amd", "lib", "random_fasta")
+    a, b, c = (str(tmp_path / x) for x in ("a.fsa", "b.fsa", "c.fsa"))
+    subprocess.run([exe, a], check=True)
+    subprocess.run([exe, b], check=True)
+    ref = open(os.path.join(DATA, "FASTA_files", "random_FASTA.fsa")).read().splitlines()
+    got = open(a).read().splitlines()
+    assert [len(x) for x in got] == [len(x) for x in ref]
+    assert [x for x in got if x.startswith(">")] == [x for x in ref if x.startswith(">")]
+    assert open(a).read() == open(b).read()
+    subprocess.run([exe, c, "500", "0", "900", "7"], check=True)
+    fa = msv.FASTA_protein_sequences(c)
+    lens = np.diff(fa.offsets.astype(np.int64))
+    assert len(fa) == 500 and fa.rejected == 0 and lens.min() >= 0 and lens.max() <= 900
