@@ -291,9 +291,12 @@ def main():
 
     # Informational: the host-buffer C-ABI path (pageable H2D copy + kernel + D2H), i.e. the
     # PCIe-inclusive rate; never the headline value.
-    t_h = time.perf_counter()
-    host_scores = engine.score_batch(codes=codes, offsets=offsets)
-    host_api_s = time.perf_counter() - t_h
+    host_scores = engine.score_batch(codes=codes, offsets=offsets)  # first call allocates its staging
+    host_api_s = 1e30
+    for _ in range(2):
+        t_h = time.perf_counter()
+        host_scores = engine.score_batch(codes=codes, offsets=offsets)
+        host_api_s = min(host_api_s, time.perf_counter() - t_h)
     ok = ok and ok_pinned and bool(np.array_equal(host_scores.view(np.uint32), scores.view(np.uint32)))
     total_residues = residues_all
     value = total_residues * args.steps / elapsed / 1e6  # M residues / s, whole job
