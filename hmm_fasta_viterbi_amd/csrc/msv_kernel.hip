@@ -138,6 +138,11 @@ constexpr int residue_prefetch() {
     return S <= 16 ? 6 : (S <= 40 ? 3 : 1);
 }
 
+// J and C are kept as PER-LANE partials: J_l = max(J_l' + loop, Elane + tEJ) with Elane the max over
+// the lane's own states.  Because max is exact and fl() is monotone, max_l J_l equals the
+// reference's J = max(J' + loop, E + tEJ) at every row (induction on the row), so the group-wide
+// E is never formed per row; the group max is taken only when B needs J (below) and once at the
+// end of the sequence for C.
 template <int S, int RPF_ = residue_prefetch<S>()>
 struct Stream {
     static constexpr int RPF = RPF_;
@@ -186,6 +191,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
 
     const uint8_t* __restrict__ res = a.residues;
     const float trBMk = a.tr_B_Mk, tEC = a.tr_E_C, tEJ = a.tr_E_J;
+    const bool sameEJ = __float_as_uint(tEC) == __float_as_uint(tEJ);  // wave-uniform (SGPR)
 
     uint32_t rows_done = 0;  // rows issued by this wave (diagnostics)
     // Work distribution: a group takes its first sequence when it starts; the index of its next
@@ -221,7 +227,9 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             atomicOr(a.errors, kErrTooLong);
         }
         const bool run = !retire && !empty && !too_long;
-        const float2 lm = run ? a.lentab[L] : make_float2(0.f, 0.f);
+        // A retired or junk stream runs with move = -inf: B = Bt = -inf keeps its rows at -inf, so
+        // its J partials never reach N and never force the epilogue's group reduction.
+        const float2 lm = run ? a.lentab[L] : make_float2(0.f, NINF);
         st.loop = lm.x;
         st.move = lm.y;
         st.seq = s;
@@ -267,10 +275,14 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         rc.ep = ep;
         rc.Bt = st.B + trBMk;
         rc.nbr = shift_in<G>(st.M[S - 1], NINF);
-        rc.p0 = NINF;
-        rc.p1 = NINF;
-        rc.p2 = NINF;
-        rc.p3 = NINF;
+        // p0/p1 start from the row's first chunk (a plain max, no -inf seed); the EXP & 4 timing
+        // experiment seeds all four
+        if constexpr (EXP & 4) {
+            rc.p0 = NINF;
+            rc.p1 = NINF;
+            rc.p2 = NINF;
+            rc.p3 = NINF;
+        }
         if constexpr (!XROW) fill_ring(rc, ep);
     };
     // One float4 chunk (states 4c+1 .. 4c+4 of the lane), highest state first so M[k-1] is still
@@ -300,17 +312,33 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
                 "v_max_f32 %1, %2, %4"
                 : "+v"(st.M[k + 3]), "+v"(st.M[k + 2]), "+v"(st.M[k + 1])
                 : "v"(st.M[k]), "v"(rc.Bt));
-            asm volatile(
-                "v_add_f32 %0, %8, %0\n\t"
-                "v_max_f32 %2, %3, %7\n\t"
-                "v_add_f32 %1, %9, %1\n\t"
-                "v_max_f32 %3, %6, %7\n\t"
-                "v_add_f32 %2, %10, %2\n\t"
-                "v_max3_f32 %4, %4, %0, %1\n\t"
-                "v_add_f32 %3, %11, %3\n\t"
-                "v_max3_f32 %5, %5, %2, %3"
-                : "+v"(st.M[k + 3]), "+v"(st.M[k + 2]), "+v"(st.M[k + 1]), "+v"(st.M[k]), "+v"(rc.p0), "+v"(rc.p1)
-                : "v"(mprev), "v"(rc.Bt), "v"(ev.w), "v"(ev.z), "v"(ev.y), "v"(ev.x));
+            if constexpr (c == C4 - 1) {  // the row's first chunk starts the E partials (no -inf seed)
+                asm volatile(
+                    "v_add_f32 %0, %8, %0\n\t"
+                    "v_max_f32 %2, %3, %7\n\t"
+                    "v_add_f32 %1, %9, %1\n\t"
+                    "v_max_f32 %3, %6, %7\n\t"
+                    "v_add_f32 %2, %10, %2\n\t"
+                    "v_max_f32 %4, %0, %1\n\t"
+                    "v_add_f32 %3, %11, %3\n\t"
+                    "v_max_f32 %5, %2, %3"
+                    : "+v"(st.M[k + 3]), "+v"(st.M[k + 2]), "+v"(st.M[k + 1]), "+v"(st.M[k]), "=&v"(rc.p0),
+                      "=&v"(rc.p1)
+                    : "v"(mprev), "v"(rc.Bt), "v"(ev.w), "v"(ev.z), "v"(ev.y), "v"(ev.x));
+            } else {
+                asm volatile(
+                    "v_add_f32 %0, %8, %0\n\t"
+                    "v_max_f32 %2, %3, %7\n\t"
+                    "v_add_f32 %1, %9, %1\n\t"
+                    "v_max_f32 %3, %6, %7\n\t"
+                    "v_add_f32 %2, %10, %2\n\t"
+                    "v_max3_f32 %4, %4, %0, %1\n\t"
+                    "v_add_f32 %3, %11, %3\n\t"
+                    "v_max3_f32 %5, %5, %2, %3"
+                    : "+v"(st.M[k + 3]), "+v"(st.M[k + 2]), "+v"(st.M[k + 1]), "+v"(st.M[k]), "+v"(rc.p0),
+                      "+v"(rc.p1)
+                    : "v"(mprev), "v"(rc.Bt), "v"(ev.w), "v"(ev.z), "v"(ev.y), "v"(ev.x));
+            }
             return;
         }
         // (EXP & 2048: timing-only A/B, the compiler-scheduled C++ form of the same chunk)
@@ -325,6 +353,9 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         if constexpr ((EXP & 4) && (c & 1)) {  // 4 accumulators: half-length E dependency chains
             rc.p2 = fmaxf(fmaxf(rc.p2, st.M[k + 3]), st.M[k + 2]);
             rc.p3 = fmaxf(fmaxf(rc.p3, st.M[k + 1]), st.M[k]);
+        } else if constexpr (c == C4 - 1 && !(EXP & 4)) {  // first chunk of the row: no -inf seed
+            rc.p0 = fmaxf(st.M[k + 3], st.M[k + 2]);
+            rc.p1 = fmaxf(st.M[k + 1], st.M[k]);
         } else {
             rc.p0 = fmaxf(fmaxf(rc.p0, st.M[k + 3]), st.M[k + 2]);
             rc.p1 = fmaxf(fmaxf(rc.p1, st.M[k + 1]), st.M[k]);
@@ -333,13 +364,23 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // Row epilogue: E over the group, the specials (MSV_HMM.cpp:107-110), cursor advance.
     auto epilogue = [&](St& st, auto& rc) {
         const float Elane = (EXP & 4) ? fmaxf(fmaxf(rc.p0, rc.p1), fmaxf(rc.p2, rc.p3)) : fmaxf(rc.p0, rc.p1);
+        // Per-lane partials (see Stream): J_l, and C_l unless C == J (tr_E_C == tr_E_J, which is
+        // always the case for the reference's nu = 2, MSV_HMM.cpp:49-53: then the C and J
+        // recurrences are identical and C is read from J at the end).
+        const float EJ = Elane + tEJ;
+        st.J = fmaxf(st.J + st.loop, EJ);
+        if (!sameEJ) st.C = fmaxf(st.C + st.loop, Elane + tEC);
+        st.N = st.N + st.loop;
+        // B = max(N, J) + move needs the group's J = max_l J_l only if some J_l >= N; otherwise
+        // max(N, J) == N exactly.  On random-like sequences J stays below N, so the per-row E/J
+        // reduction across lanes (DPP butterfly) leaves the row's dependency chain.
         // (G = 64: a row_bcast:15/31 + v_readlane reduction to an SGPR measured 13% slower on
         // 2405.hmm than the permlane swaps -- the SGPR round trip stalls the row)
-        const float E = group_max<G>(Elane);
-        st.J = fmaxf(st.J + st.loop, E + tEJ);
-        st.C = fmaxf(st.C + st.loop, E + tEC);
-        st.N = st.N + st.loop;
-        st.B = fmaxf(st.N, st.J) + st.move;
+        if (__builtin_expect(__any(st.J >= st.N), 0)) {
+            st.B = fmaxf(st.N, group_max<G>(st.J)) + st.move;
+        } else {
+            st.B = st.N + st.move;
+        }
         ++st.pos;
         --st.rows_left;
 #pragma unroll
@@ -347,7 +388,10 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         st.r[St::RPF - 1] = rc.rnext;
     };
     auto finish = [&](St& st) {
-        const float sc = st.C + st.move;  // dp.back()[C] + tr_move (MSV_HMM.cpp:112)
+        // Every lane of the group is here (rows_left is group-uniform), so the group reduction of
+        // the C partials reads only active lanes of the same group.
+        const float C = group_max<G>(sameEJ ? st.J : st.C);
+        const float sc = C + st.move;  // dp.back()[C] + tr_move (MSV_HMM.cpp:112)
         if (leader && !st.junk) {
             a.scores[st.seq] = sc;
             if (!(sc <= 3.402823466e38f)) atomicOr(a.errors, kErrBadResidue);  // poison row hit

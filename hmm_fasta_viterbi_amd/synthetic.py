@@ -72,3 +72,43 @@ def write_hmm(path: str, leng: int, seed: int) -> None:
     out.append("//")
     with open(path, "w") as f:
         f.write("\n".join(out) + "\n")
+
+
+def homolog_batch(match_emissions: np.ndarray, seed: int, n: int, lmin: int, lmax: int,
+                  mutate: float = 0.1) -> tuple[np.ndarray, np.ndarray]:
+    """Sequences EMITTED by the profile's match states (a run of consecutive states from a random
+    start, each residue drawn from that state's match-emission distribution, a `mutate` fraction
+    replaced by uniform residues), wrapped in uniform flanks.  They score far above random ones,
+    so the DP's J state overtakes N (B = max(N, J) + move then depends on J) -- the rows the
+    kernel's J-reduction path handles.  `match_emissions`: Profile_HMM.match_emissions, [M][20]
+    with node 0 all zeros."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    probs = np.asarray(match_emissions, np.float64)[1:]
+    leng = probs.shape[0]
+    cdf = np.cumsum(probs / probs.sum(axis=1, keepdims=True), axis=1)
+    seqs = []
+    for _ in range(n):
+        L = int(rng.integers(lmin, lmax + 1))
+        core = min(L, leng, int(rng.integers(max(1, L // 2), L + 1)))
+        start = int(rng.integers(0, leng - core + 1))
+        u = rng.random(core)
+        emitted = np.minimum((cdf[start:start + core] < u[:, None]).sum(axis=1), 19).astype(np.uint8)
+        flip = rng.random(core) < mutate
+        emitted[flip] = rng.integers(0, 20, size=int(flip.sum()), dtype=np.uint8)
+        left = int(rng.integers(0, L - core + 1))
+        seq = rng.integers(0, 20, size=L, dtype=np.uint8)
+        seq[left:left + core] = emitted
+        seqs.append(seq)
+    offsets = np.zeros(n + 1, np.uint64)
+    np.cumsum([len(s) for s in seqs], out=offsets[1:])
+    codes = np.concatenate(seqs) if seqs else np.zeros(0, np.uint8)
+    return codes, offsets
+
+
+def concat_batches(*batches: tuple[np.ndarray, np.ndarray]) -> tuple[np.ndarray, np.ndarray]:
+    """Concatenate CSR batches (codes, offsets) in order."""
+    codes = np.concatenate([c for c, _ in batches])
+    lens = np.concatenate([np.diff(o) for _, o in batches]).astype(np.uint64)
+    offsets = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=offsets[1:])
+    return codes, offsets

@@ -11,7 +11,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 import hmm_fasta_viterbi_amd as msv
-from hmm_fasta_viterbi_amd.synthetic import random_batch
+from hmm_fasta_viterbi_amd.synthetic import concat_batches, homolog_batch, random_batch
 from oracle_lib import GOLD, PROFILES, ROOT, OracleProfile, bits, profile_path, read_golden_tsv
 
 _engines = {}
@@ -201,7 +201,7 @@ def test_every_variant_matches_oracle(tmp_path):
         paths.append(str(tmp_path / f"syn{leng}.hmm"))
         write_hmm(paths[-1], leng, leng)
     lengs = {p: msv.Profile_HMM(p).model_length - 1 for p in paths}
-    codes, offsets = random_batch(21, 48, 0, 400)
+    codes0, offsets0 = random_batch(21, 48, 0, 400)
     by_prof = {}
     for name in msv.MSV_HMM.variants():
         if name.startswith("exp"):
@@ -212,6 +212,10 @@ def test_every_variant_matches_oracle(tmp_path):
             by_prof.setdefault(max(fits, key=lambda p: lengs[p]), []).append(name)
     assert sum(len(v) for v in by_prof.values()) >= 40
     for prof, names in by_prof.items():
+        # random sequences (J stays below N) interleaved with sequences emitted by the profile
+        # (J overtakes N: the kernel's group reduction of J for B runs on those rows)
+        hc, ho = homolog_batch(msv.Profile_HMM(prof).match_emissions, 22, 24, 0, 400)
+        codes, offsets = concat_batches((codes0, offsets0), (hc, ho))
         want = OracleProfile(prof).score_batch(codes, offsets)
         e = msv.MSV_HMM(msv.Profile_HMM(prof))
         for name in names:
@@ -566,3 +570,84 @@ def test_score_batch_multi_concurrent_length_table_growth():
     assert np.array_equal(bits(got), bits(OracleProfile("100").score_batch(codes, offsets)))
     for e in engines:
         e.close()
+
+
+def _homolog_j_rows(codes, offsets, scores):
+    """How many sequences end with J >= N (so B took J at least on the last row)."""
+    L = np.diff(offsets).astype(np.float64)
+    ok = L > 0
+    move = np.log(3.0 / (L[ok] + 3.0))
+    return int(((scores[ok] - move) >= L[ok] * np.log(L[ok] / (L[ok] + 3.0)) + 1e-3).sum())
+
+
+@pytest.mark.parametrize("prof", ["100", "500", "1400", "1901", "2405"])
+def test_homolog_sequences_match_oracle(prof):
+    """Sequences emitted by the profile itself (high scores: J >= N on many rows, so B depends on
+    the group-wide J), mixed with random ones in the same waves, under the automatic variant and
+    the latency plan's batch sizes, bitwise against the oracle."""
+    e = engine(prof)
+    hc, ho = homolog_batch(msv.Profile_HMM(profile_path(prof)).match_emissions, 5, 300, 1, 700)
+    rc, ro = random_batch(6, 300, 1, 700)
+    codes, offsets = concat_batches((hc, ho), (rc, ro))
+    want = OracleProfile(prof).score_batch(codes, offsets)
+    assert _homolog_j_rows(hc, ho, want[:300]) > 150, "homolog batch no longer exercises J >= N"
+    got = e.score_batch(codes=codes, offsets=offsets)
+    assert np.array_equal(bits(got), bits(want))
+    small = e.score_batch(codes=hc[: int(ho[8])], offsets=ho[:9])  # latency-plan sized batch
+    assert np.array_equal(bits(small), bits(want[:8]))
+
+
+def _numpy_msv(es, tBMk, tEC, tEJ, codes, offsets):
+    """float32 restatement of MSV_HMM::run_on_sequence (MSV_HMM.cpp:74-113) with free tr_E_C /
+    tr_E_J (the reference fixes both to logf(0.5f)); every add is one IEEE float32 op in the
+    reference's order, max is exact, so results are bit-comparable."""
+    f = np.float32
+    out = np.zeros(len(offsets) - 1, np.float32)
+    for s in range(len(offsets) - 1):
+        seq = codes[int(offsets[s]):int(offsets[s + 1])]
+        L = len(seq)
+        loop, move = msv.sequence_transitions(L)
+        loop, move = f(loop), f(move)
+        M = np.full(es.shape[1], -np.inf, np.float32)
+        J = C = f(-np.inf)
+        N, B = f(0.0), move
+        for r in seq:
+            Bt = f(B + f(tBMk))
+            newM = np.full_like(M, -np.inf)
+            newM[1:] = es[r, 1:] + np.maximum(M[:-1], Bt)
+            M = newM
+            E = M[1:].max()
+            J = max(f(J + loop), f(E + f(tEJ)))
+            C = max(f(C + loop), f(E + f(tEC)))
+            N = f(N + loop)
+            B = f(max(N, J) + move)
+        out[s] = f(C + move) if L else -np.inf
+    return out
+
+
+def test_distinct_tr_E_C_and_tr_E_J():
+    """The C-ABI accepts tr_E_C != tr_E_J (no reference profile has that): the kernel then keeps
+    separate C partials instead of reading C from J."""
+    import ctypes as C
+    from hmm_fasta_viterbi_amd import _native
+    L = _native.lib()
+    h = msv.Profile_HMM(profile_path("100"))
+    es, tBMk, _, _ = h.msv_scores()
+    es = np.ascontiguousarray(es, np.float32)
+    hc, ho = homolog_batch(h.match_emissions, 9, 12, 1, 60)
+    rc, ro = random_batch(10, 12, 0, 60)
+    codes, offsets = concat_batches((hc, ho), (rc, ro))
+    for tEC, tEJ in ((-0.3, -1.2), (-2.0, -0.1)):
+        want = _numpy_msv(es, tBMk, tEC, tEJ, codes, offsets)
+        p = C.c_void_p()
+        assert L.msv_profile_create(0, es.ctypes.data, es.shape[1], tBMk, tEC, tEJ, C.byref(p)) == 0
+        try:
+            got = np.zeros(len(offsets) - 1, np.float32)
+            assert L.msv_score_batch(p, codes.ctypes.data, offsets.ctypes.data, len(got), got.ctypes.data, None) == 0
+        finally:
+            L.msv_profile_destroy(p)
+        assert np.array_equal(bits(got), bits(want)), (tEC, tEJ)
+    # and the numpy restatement itself agrees with the oracle at the reference's constants
+    _, _, tEC0, tEJ0 = h.msv_scores()
+    assert np.array_equal(bits(_numpy_msv(es, tBMk, tEC0, tEJ0, codes, offsets)),
+                          bits(OracleProfile("100").score_batch(codes, offsets)))
