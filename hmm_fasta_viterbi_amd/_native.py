@@ -9,7 +9,9 @@ import ctypes as C
 import os
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libmsv_hip.so")
+# MSV_LIB_PATH: another build of the same library (tools/ab.py compares two builds in one process
+# run); unset in every test and product run.
+LIB_PATH = os.environ.get("MSV_LIB_PATH") or os.path.join(LIB_DIR, "libmsv_hip.so")
 
 STATUS = {
     0: "MSV_OK",

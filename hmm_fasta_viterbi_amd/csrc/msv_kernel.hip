@@ -63,23 +63,26 @@ constexpr int DPP_ROW_HMIRROR = 0x141; // row_half_mirror
 constexpr int DPP_ROW_BCAST15 = 0x142; // row_bcast:15
 
 // M_{j-1} for the first state of each lane: the last state of the previous lane of the same
-// group; -inf (the dummy M0 column, MSV_HMM.cpp:86) for the first lane of a group.
+// group; -inf (the dummy M0 column, MSV_HMM.cpp:86) for the first lane of a group.  `old` supplies
+// the lanes the shift does not write: -inf there (G < 16: any value, the -inf is selected here).
+// For G >= 16 the caller passes the previous result back in, so those lanes keep the -inf written
+// once at start and no per-row -inf copy is needed.
 template <int G>
-__device__ __forceinline__ float shift_in(float last, float ninf) {
+__device__ __forceinline__ float shift_in(float last, float old) {
     if constexpr (G < 16) {
         static_assert(G == 4 || G == 8, "G must be 4, 8, 16, 32 or 64");
-        const float v = dpp<DPP_ROW_SHR1>(ninf, last);
-        return (threadIdx.x & (G - 1)) == 0 ? ninf : v;  // first lane of each group inside the row
+        const float v = dpp<DPP_ROW_SHR1>(old, last);
+        return (threadIdx.x & (G - 1)) == 0 ? -__builtin_inff() : v;  // first lane of each group
     } else if constexpr (G == 16) {
-        return dpp<DPP_ROW_SHR1>(ninf, last);
+        return dpp<DPP_ROW_SHR1>(old, last);
     } else if constexpr (G == 32) {
         // rows 1 and 3 first receive lane 15 of rows 0 and 2; row_shr:1 then fills every lane
         // except the first of each row, which keeps that broadcast (or -inf for rows 0 and 2).
-        float v = dpp<DPP_ROW_BCAST15, 0xA>(ninf, last);
+        float v = dpp<DPP_ROW_BCAST15, 0xA>(old, last);
         return dpp<DPP_ROW_SHR1>(v, last);
     } else {
         static_assert(G == 64, "G must be 16, 32 or 64");
-        float v = dpp<DPP_ROW_BCAST15, 0xE>(ninf, last);  // rows 1-3 get lane 15 of the row before
+        float v = dpp<DPP_ROW_BCAST15, 0xE>(old, last);  // rows 1-3 get lane 15 of the row before
         return dpp<DPP_ROW_SHR1>(v, last);
     }
 }
@@ -148,7 +151,11 @@ struct Stream {
     static constexpr int RPF = RPF_;
     float M[S];
     float J, C, N, B, loop, move;
-    uint32_t pos, endpos, rows_left, seq, half;  // half: rows_left at which to fetch the next index
+    float nbr;        // M_{j-1} of the lane's first state; lane 0 of each DPP row is never written
+                      // by the shift (invalid source), so it keeps the -inf set once at start
+    // pos: residue of the current row; endpos: last residue (prefetch clamp); endp: pos after the
+    // last row; ev: pos at which the next event fires (the half-way index fetch, then endp)
+    uint32_t pos, endpos, endp, ev, seq;
     uint32_t r[RPF];  // residue codes of the next RPF rows (r[0] = this row)
     bool active;
     bool junk;        // current "sequence" is an empty/too-long record: discard its row
@@ -235,9 +242,10 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         st.seq = s;
         st.pos = run ? static_cast<uint32_t>(o0) : 0u;
         st.endpos = run ? static_cast<uint32_t>(o1 - 1) : 0u;
-        st.rows_left = retire ? 0xFFFFFFFFu : (run ? static_cast<uint32_t>(L) : 1u);
-        // half == 0xFFFFFFFF equals the initial rows_left of a retired stream: never matched again
-        st.half = run ? static_cast<uint32_t>(L >> 1) : 0xFFFFFFFFu;
+        // a junk stream ends after its one row; a retired one never (pos cannot reach 2^32 - 1)
+        st.endp = retire ? 0xFFFFFFFFu : (run ? static_cast<uint32_t>(o1) : 1u);
+        // the next index is fetched after L - L/2 rows (equal to endp when L == 1: begin fetches it)
+        st.ev = run ? static_cast<uint32_t>(o1 - (L >> 1)) : st.endp;
 #pragma unroll
         for (int k = 0; k < S; ++k) st.M[k] = NINF;
         st.J = NINF;
@@ -249,13 +257,22 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
 #pragma unroll
         for (int q = 0; q < St::RPF; ++q) st.r[q] = res[min(st.pos + q, st.endpos)];
     };
-    auto init = [&](St& st) { begin(st); };
+    auto init = [&](St& st) {
+        st.nbr = NINF;
+        begin(st);
+    };
     // Row prologue: next residue prefetch, emission row pointer, Bt, the j-1 neighbour, ring fill.
+    // LDS row of residue code r for this lane (codes >= 20 -> the poison row).  (A hand-written
+    // v_min_sdwa + v_mad_u32_u24 form of this address, and pinning the prefetched residue as a
+    // 32-bit value, each measured 2-4% slower on 1400.hmm: they move the residue-load wait.)
+    auto lds_row = [&](uint32_t r) -> const float4* {
+        return &tab[min(r, static_cast<uint32_t>(kPoisonRow)) * ROW_F4 + gl];
+    };
     auto row_ptr = [&](St& st) -> const float4* {
-        const uint32_t rr = min(st.r[0], static_cast<uint32_t>(kPoisonRow));
         if constexpr (!BIG) {
-            return &tab[rr * ROW_F4 + gl];
+            return lds_row(st.r[0]);
         } else {
+            const uint32_t rr = min(st.r[0], static_cast<uint32_t>(kPoisonRow));
             return (rr < static_cast<uint32_t>(LDS_ROWS)) ? &tab[rr * ROW_F4 + gl] : &a.etab[rr * ROW_F4 + gl];
         }
     };
@@ -274,7 +291,12 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         }
         rc.ep = ep;
         rc.Bt = st.B + trBMk;
-        rc.nbr = shift_in<G>(st.M[S - 1], NINF);
+        if constexpr (G >= 16) {
+            st.nbr = shift_in<G>(st.M[S - 1], st.nbr);
+            rc.nbr = st.nbr;
+        } else {
+            rc.nbr = shift_in<G>(st.M[S - 1], NINF);
+        }
         // p0/p1 start from the row's first chunk (a plain max, no -inf seed); the EXP & 4 timing
         // experiment seeds all four
         if constexpr (EXP & 4) {
@@ -369,7 +391,10 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         // recurrences are identical and C is read from J at the end).
         const float EJ = Elane + tEJ;
         st.J = fmaxf(st.J + st.loop, EJ);
-        if (!sameEJ) st.C = fmaxf(st.C + st.loop, Elane + tEC);
+        if (!sameEJ) {
+            st.C = fmaxf(st.C + st.loop, Elane + tEC);
+            asm volatile("" ::: "memory");  // keep a real (scalar) branch, not a per-row select
+        }
         st.N = st.N + st.loop;
         // B = max(N, J) + move needs the group's J = max_l J_l only if some J_l >= N; otherwise
         // max(N, J) == N exactly.  On random-like sequences J stays below N, so the per-row E/J
@@ -382,15 +407,17 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             st.B = st.N + st.move;
         }
         ++st.pos;
-        --st.rows_left;
 #pragma unroll
         for (int q = 0; q + 1 < St::RPF; ++q) st.r[q] = st.r[q + 1];
         st.r[St::RPF - 1] = rc.rnext;
     };
     auto finish = [&](St& st) {
-        // Every lane of the group is here (rows_left is group-uniform), so the group reduction of
+        // Every lane of the group is here (pos == endp is group-uniform), so the group reduction of
         // the C partials reads only active lanes of the same group.
-        const float C = group_max<G>(sameEJ ? st.J : st.C);
+        // (the copy of J is opaque so the compiler cannot hoist this select into every row)
+        float csrc = st.C;
+        if (sameEJ) asm volatile("v_mov_b32 %0, %1" : "=v"(csrc) : "v"(st.J));
+        const float C = group_max<G>(csrc);
         const float sc = C + st.move;  // dp.back()[C] + tr_move (MSV_HMM.cpp:112)
         if (leader && !st.junk) {
             a.scores[st.seq] = sc;
@@ -426,7 +453,9 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         epilogue(st, rc);
     };
 
-    while (__any(D == 2 ? (s0.active || s1.active) : s0.active)) {
+    // Wave-uniform loop condition, refreshed only when a stream finishes.
+    bool live = __any(D == 2 ? (s0.active || s1.active) : s0.active);
+    while (live) {
         if constexpr (BIG && G == 64 && (EXP & 256)) {
             // (timing-only: vector row index, all rows from LDS, no readfirstlane -> wrong scores)
             RowCtx<PF> c0;
@@ -456,7 +485,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
                 ((chunk(s0, xr, std::integral_constant<int, C4 - 1 - I>{})), ...);
             }(std::make_integer_sequence<int, C4>{});
             // s0.r[1] is the residue of the next row (discarded if this row ends the sequence)
-            fill_ring(xr, &tab[min(s0.r[1], static_cast<uint32_t>(kPoisonRow)) * ROW_F4 + gl]);
+            fill_ring(xr, lds_row(s0.r[1]));
             epilogue(s0, xr);
         } else if constexpr (D == 1) {
             RowCtx<PF> c0;
@@ -474,18 +503,29 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             epilogue(s0, c0);
             epilogue(s1, c1);
         }
-        if (s0.rows_left == s0.half && pending == kNone)
-            pending = group_take<G>(a.counter, leader, lane);
-        if constexpr (D == 2) {
-            if (s1.rows_left == s1.half && pending == kNone)
-                pending = group_take<G>(a.counter, leader, lane);
-        }
-        if (s0.rows_left == 0) {
-            finish(s0);
-            if constexpr (XROW) fill_ring(xr, row_ptr(s0));
-        }
-        if constexpr (D == 2) {
-            if (s1.rows_left == 0) finish(s1);
+        // Events (one compare per stream and row; the handling is rare and wave-uniformly skipped):
+        // the half-way fetch of the next index, then the end of the sequence.  (G = 64: the cursor
+        // is wave-uniform and the compares are scalar; there the guard made the compiler copy the
+        // whole DP row at the loop latch, +12% per row on 2405.hmm, so it is left out.)
+        if (G == 64 || __any(D == 2 ? (s0.pos == s0.ev || s1.pos == s1.ev) : s0.pos == s0.ev)) {
+            if (s0.pos == s0.ev && s0.ev != s0.endp) {
+                if (pending == kNone) pending = group_take<G>(a.counter, leader, lane);
+                s0.ev = s0.endp;
+            }
+            if constexpr (D == 2) {
+                if (s1.pos == s1.ev && s1.ev != s1.endp) {
+                    if (pending == kNone) pending = group_take<G>(a.counter, leader, lane);
+                    s1.ev = s1.endp;
+                }
+            }
+            if (s0.pos == s0.endp) {
+                finish(s0);
+                if constexpr (XROW) fill_ring(xr, row_ptr(s0));
+            }
+            if constexpr (D == 2) {
+                if (s1.pos == s1.endp) finish(s1);
+            }
+            live = __any(D == 2 ? (s0.active || s1.active) : s0.active);
         }
         ++rows_done;
     }
