@@ -155,18 +155,21 @@ def pmc_traffic(config: str):
 
 
 def issue_ceiling_tcells():
-    """Measured instruction-mix ceiling of the cell update (profiles/r01_micro_cell_mix.jsonl:
-    tools/micro/cell_mix.hip, the kernel's exact per-chunk mix 4 v_max + 4 v_add + 2 v_max3 with no
-    memory and no per-row work, 4 waves/SIMD): cells/ns/SIMD x 1024 SIMDs -> T cells/s."""
-    path = os.path.join(ROOT, "profiles", "r01_micro_cell_mix.jsonl")
+    """Measured instruction-issue ceiling of the cell update as the kernel issues it
+    (profiles/r01_micro_row_sched.jsonl: tools/micro/row_sched.hip, one row of the kernel's exact
+    per-chunk ops -- 4 v_max + 4 v_add + 2 v_max3 per 4 cells, in the kernel's interleaved order
+    and with its real dependencies -- with no memory and no per-row work, 4 waves/SIMD; best run):
+    cells/ns/SIMD x 1024 SIMDs -> T cells/s."""
+    path = os.path.join(ROOT, "profiles", "r01_micro_row_sched.jsonl")
     if not os.path.exists(path):
         return None
+    best = None
     with open(path) as f:
         for line in f:
             d = json.loads(line)
-            if d["mix"].startswith("A_") and d["waves_per_simd"] == 4:
-                return d["cells_per_ns_per_simd"] * 1024 / 1000.0
-    return None
+            if d["sched"].startswith("D_max3_interleaved"):
+                best = max(best or 0.0, d["cells_per_ns_per_simd"])
+    return None if best is None else best * 1024 / 1000.0
 
 
 def main():
@@ -349,8 +352,9 @@ def main():
                 "tcells_per_s": round(ceiling, 3),
                 "achieved_tcells_per_s": round(cells_per_launch / (kernel_ms * 1e-3) / 1e12, 3),
                 "frac": round(cells_per_launch / (kernel_ms * 1e-3) / 1e12 / ceiling, 4),
-                "source": "profiles/r01_micro_cell_mix.jsonl (measured: v_max/v_max3 issue at half the "
-                          "v_add rate, so 2.5 VALU/cell cannot reach the nominal peak)",
+                "source": "profiles/r01_micro_row_sched.jsonl (measured: v_max/v_max3 issue at half the "
+                          "v_add rate, so 2.5 VALU/cell cannot reach the nominal peak; kernel's interleaved "
+                          "chunk order, no per-row work)",
             },
             "hbm": {
                 "algorithmic_bytes_per_launch": alg_bytes,
