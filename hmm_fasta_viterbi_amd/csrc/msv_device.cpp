@@ -86,9 +86,11 @@ msv_status hip_status(hipError_t e) {
 // specials/reduction, times the lanes a sequence occupies.  A BIG table costs little with one
 // sequence per wave (G = 64: wave-uniform LDS/L2 row split) and a lot with 2-4 sequences per wave
 // (generic loads with per-lane address selects); measured on 2405.hmm: 7.4 vs 10.5 ms.
+// A split table (one sequence per wave, the lane's last S - SA states read from L2 every row) costs
+// two more DPP moves per row and no class branch.
 double variant_cost(const msvk::Variant& v) {
     const double big = !v.big ? 1.0 : (v.G == 64 ? 1.03 : 1.6);
-    const double row = v.G == 64 ? 36.0 : 26.0;  // + permlane32 step, scalar sequence bookkeeping
+    const double row = v.G == 64 ? (v.sa ? 38.0 : 36.0) : 26.0;  // + permlane32 step, scalar bookkeeping
     return (2.5 * v.S + row) * v.G * big * (v.pf == 2 ? 1.0 : 1.05) * (v.streams == 2 ? 1.15 : 1.0);
 }
 
@@ -167,22 +169,35 @@ struct msv_profile {
 // Lays the MSV table out for variant v and uploads it:
 // [row r][chunk c][lane gl] float4 = e[r][gl*S + 4c + 1 .. +4]; states beyond LENG are -inf
 // (never win a max); row 20 is the +inf poison row for codes >= 20.
+// Split variants (v->sa > 0, G = 64): an A table [20 rows][SA/4][G] float4 (lane gl's states gl*SA + 1 ..,
+// staged in LDS) followed by a B table [21 rows][(S-SA)/2][G] float2 (lane gl's states
+// 64*SA + gl*(S-SA) + 1 .., read from L2; row 20 = poison).
 static msv_status install_plan(msv_profile* p, const msvk::Variant* v, Plan& plan) {
     const uint32_t model_length = p->model_length, R = model_length - 1;
     const int G = v->G, S = v->S, C4 = S / 4;
-    std::vector<float> tab(static_cast<size_t>(msvk::kTableRows) * C4 * G * 4);
     const float ninf = -std::numeric_limits<float>::infinity();
     const float pinf = std::numeric_limits<float>::infinity();
-    for (int r = 0; r < msvk::kTableRows; ++r)
-        for (int c = 0; c < C4; ++c)
-            for (int gl = 0; gl < G; ++gl)
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t j = static_cast<uint32_t>(gl * S + 4 * c + q + 1);  // match state 1..
-                    float val;
-                    if (r == msvk::kPoisonRow) val = pinf;
-                    else val = (j <= R) ? p->emission_scores[static_cast<size_t>(r) * model_length + j] : ninf;
-                    tab[((static_cast<size_t>(r) * C4 + c) * G + gl) * 4 + q] = val;
-                }
+    std::vector<float> tab;
+    // one [rows][chunks][G] block of `width`-float chunks (float4, or float2 for a split B table) whose
+    // lane gl, chunk c, slot q holds state first + gl*span + width*c + q
+    auto block = [&](int rows, int chunks, uint32_t first, int span, int width) {
+        for (int r = 0; r < rows; ++r)
+            for (int c = 0; c < chunks; ++c)
+                for (int gl = 0; gl < G; ++gl)
+                    for (int q = 0; q < width; ++q) {
+                        const uint32_t j = first + static_cast<uint32_t>(gl * span + width * c + q);  // state 1..
+                        float val;
+                        if (r == msvk::kPoisonRow) val = pinf;
+                        else val = (j <= R) ? p->emission_scores[static_cast<size_t>(r) * model_length + j] : ninf;
+                        tab.push_back(val);
+                    }
+    };
+    if (v->sa > 0) {
+        block(msvk::kAminoAcids, v->sa / 4, 1, v->sa, 4);
+        block(msvk::kTableRows, (S - v->sa) / 2, static_cast<uint32_t>(G * v->sa + 1), S - v->sa, 2);
+    } else {
+        block(msvk::kTableRows, C4, 1, S, 4);
+    }
     float4* d = nullptr;
     MSV_HIP(hipMalloc(reinterpret_cast<void**>(&d), tab.size() * sizeof(float)));
     hipError_t e = hipMemcpy(d, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice);
@@ -435,7 +450,7 @@ msv_status msv_profile_describe(const msv_profile* p, msv_kernel_info* out) {
     out->states_per_lane = static_cast<uint32_t>(v->S);
     out->waves_per_block = static_cast<uint32_t>(v->waves);
     out->lds_rows = static_cast<uint32_t>(v->lds_rows);
-    out->lds_bytes = static_cast<uint32_t>(v->lds_rows * v->G * v->S * 4);
+    out->lds_bytes = static_cast<uint32_t>(v->lds_rows * v->G * (v->sa ? v->sa : v->S) * 4);
     out->blocks = static_cast<uint32_t>(p->main.blocks);
     out->max_length = p->lentab_n ? p->lentab_n - 1 : 0;
     out->device = p->device;

@@ -41,6 +41,7 @@ struct Variant {
     bool big;
     const void* fn;
     const char* name;
+    int sa = 0;  // split layout: states per lane staged in LDS (0 = whole table layout)
 };
 
 const Variant* variants(int* count);

@@ -61,6 +61,8 @@ constexpr int DPP_ROW_SHR1 = 0x111;    // row_shr:1
 constexpr int DPP_ROW_MIRROR = 0x140;  // row_mirror
 constexpr int DPP_ROW_HMIRROR = 0x141; // row_half_mirror
 constexpr int DPP_ROW_BCAST15 = 0x142; // row_bcast:15
+constexpr int DPP_WAVE_SHR1 = 0x138;   // wave_shr:1
+constexpr int DPP_WAVE_ROR1 = 0x13C;   // wave_ror:1
 
 // M_{j-1} for the first state of each lane: the last state of the previous lane of the same
 // group; -inf (the dummy M0 column, MSV_HMM.cpp:86) for the first lane of a group.  `old` supplies
@@ -166,25 +168,35 @@ template <int PF>
 struct RowCtx {
     static constexpr int kPF = PF;
     const float4* ep;
-    float Bt, nbr, p0, p1, p2, p3;
+    float Bt, nbr, nbrB, p0, p1, p2, p3;  // nbrB: split layout, neighbour of the lane's first B state
     uint32_t rnext;  // residue code RPF rows ahead
     float4 ring[PF];
 };
 
-template <int G, int S, int WAVES, int PF, bool BIG, int D, int EXP = 0>
+// SA > 0 selects the SPLIT layout (one sequence per wave, G = 64): each lane's first SA states (the
+// "A block", states 1..64*SA) have all 20 residue rows in LDS, its last S - SA states (the "B block",
+// states 64*SA+1..) are read from the global table (L2) for every row -- no per-row LDS/L2 class
+// branch; the next row's B chunks are requested one row ahead.
+template <int G, int S, int WAVES, int PF, bool BIG, int D, int SA = 0, int EXP = 0>
 __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs a) {
+    constexpr bool SPLIT = SA > 0;
     // (EXP & 64: timing-only A/B, one row of residue prefetch; 2 rows measured no faster at S=88)
-    using St = Stream<S, (EXP & 64) ? 1 : residue_prefetch<S>()>;
-    static_assert(S % 4 == 0, "S must be a multiple of 4 (float4 chunks)");
+    // SPLIT needs the next row's residue one row early (B-chunk prefetch): at least 2 rows.
+    using St = Stream<S, (EXP & 64) ? 1 : ((SPLIT && residue_prefetch<S>() < 2) ? 2 : residue_prefetch<S>())>;
+    static_assert(SPLIT ? (S - SA) % 2 == 0 : S % 4 == 0, "float4 chunks (A block), float2 halves (B block)");
     static_assert(PF >= 1 && D >= 1 && D <= 2, "PF >= 1, D in {1, 2}");
+    static_assert(!SPLIT || (G == 64 && !BIG && D == 1 && SA % 4 == 0 && SA < S), "split: one sequence per wave");
     constexpr int C4 = S / 4;
-    constexpr int ROW_F4 = C4 * G;  // float4 per residue row
-    constexpr int LDS_ROWS = lds_rows_for(G, S);
+    constexpr int CA = SPLIT ? SA / 4 : C4;  // float4 chunks per lane whose emissions are staged in LDS
+    constexpr int HB = SPLIT ? (S - SA) / 2 : 0;  // SPLIT: float2 halves per lane read from the B table
+    constexpr int ROW_F4 = CA * G;           // float4 per LDS residue row
+    constexpr int ROW_B = HB * G;            // float2 per global B-table residue row
+    constexpr int LDS_ROWS = SPLIT ? kAminoAcids : lds_rows_for(G, S);
     // Cross-row emission prefetch: when the ring holds a whole row (small profiles), the NEXT row's
     // chunks are requested right after this row's last cell update, so the LDS latency hides behind
     // the E butterfly and the specials instead of stalling the start of every row.
-    constexpr bool XROW = !BIG && D == 1 && PF >= C4 && residue_prefetch<S>() >= 2;
-    static_assert(BIG == (LDS_ROWS < kTableRows), "BIG <=> table does not fit LDS");
+    constexpr bool XROW = !BIG && !SPLIT && D == 1 && PF >= C4 && residue_prefetch<S>() >= 2;
+    static_assert(SPLIT || BIG == (LDS_ROWS < kTableRows), "BIG <=> table does not fit LDS");
     __shared__ float4 tab[LDS_ROWS * ROW_F4];
 
     const float NINF = -__builtin_inff();
@@ -265,8 +277,24 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // LDS row of residue code r for this lane (codes >= 20 -> the poison row).  (A hand-written
     // v_min_sdwa + v_mad_u32_u24 form of this address, and pinning the prefetched residue as a
     // 32-bit value, each measured 2-4% slower on 1400.hmm: they move the residue-load wait.)
+    // (SPLIT: the LDS holds rows 0..19 only; codes >= 20 read row 19 there and the +inf poison row
+    // of the B table, which still makes the score +inf.)
     auto lds_row = [&](uint32_t r) -> const float4* {
-        return &tab[min(r, static_cast<uint32_t>(kPoisonRow)) * ROW_F4 + gl];
+        return &tab[min(r, static_cast<uint32_t>(SPLIT ? kAminoAcids - 1 : kPoisonRow)) * ROW_F4 + gl];
+    };
+    // SPLIT: the B table ([21][HB][G] float2: 2-state halves, so the padding past LENG stays under
+    // 2 states per lane) follows the 20 LDS rows in a.etab; the current row's B halves live in
+    // `bring`, requested one row ahead.
+    const float2* __restrict__ etabB = reinterpret_cast<const float2*>(a.etab + kAminoAcids * ROW_F4);
+    struct BRing {
+        float2 v[HB > 0 ? HB : 1];
+    } bring;
+    auto fill_b = [&](uint32_t r) {
+        if constexpr (SPLIT) {
+            const float2* bp = &etabB[min(r, static_cast<uint32_t>(kPoisonRow)) * ROW_B + gl];
+#pragma unroll
+            for (int q = 0; q < HB; ++q) bring.v[q] = bp[q * G];
+        }
     };
     auto row_ptr = [&](St& st) -> const float4* {
         if constexpr (!BIG) {
@@ -280,7 +308,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     auto fill_ring = [&](auto& rc, const float4* ep) {
         constexpr int P = std::decay_t<decltype(rc)>::kPF;
 #pragma unroll
-        for (int q = 0; q < (P < C4 ? P : C4); ++q) rc.ring[q] = ep[(C4 - 1 - q) * G];
+        for (int q = 0; q < (P < CA ? P : CA); ++q) rc.ring[q] = ep[(CA - 1 - q) * G];
     };
     auto prologue = [&](St& st, auto& rc, const float4* ep) {
         // (EXP & 32: timing-only, synthetic residues instead of the stream -> wrong scores)
@@ -291,7 +319,13 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         }
         rc.ep = ep;
         rc.Bt = st.B + trBMk;
-        if constexpr (G >= 16) {
+        if constexpr (SPLIT) {
+            // A block: lane l-1's last A state (-inf for lane 0); B block: lane l-1's last B state,
+            // and for lane 0 the last A state of lane 63 (wave_ror:1, then wave_shr:1 keeps it there)
+            st.nbr = shift_in<G>(st.M[SA - 1], st.nbr);
+            rc.nbr = st.nbr;
+            rc.nbrB = dpp<DPP_WAVE_SHR1>(dpp_perm<DPP_WAVE_ROR1>(st.M[SA - 1]), st.M[S - 1]);
+        } else if constexpr (G >= 16) {
             st.nbr = shift_in<G>(st.M[S - 1], st.nbr);
             rc.nbr = st.nbr;
         } else {
@@ -312,7 +346,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     auto chunk = [&](St& st, auto& rc, auto cc) {
         constexpr int P = std::decay_t<decltype(rc)>::kPF;
         constexpr int c = decltype(cc)::value;
-        constexpr int slot = (C4 - 1 - c) % P;
+        constexpr int slot = (CA - 1 - c) % P;
         const float4 ev = rc.ring[slot];
         // (EXP & 1: timing-only experiment, emissions not re-read -> wrong scores, never shipped)
         if constexpr (c - P >= 0 && !(EXP & 1)) rc.ring[slot] = rc.ep[(c - P) * G];
@@ -334,7 +368,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
                 "v_max_f32 %1, %2, %4"
                 : "+v"(st.M[k + 3]), "+v"(st.M[k + 2]), "+v"(st.M[k + 1])
                 : "v"(st.M[k]), "v"(rc.Bt));
-            if constexpr (c == C4 - 1) {  // the row's first chunk starts the E partials (no -inf seed)
+            if constexpr (!SPLIT && c == CA - 1) {  // the row's first chunk starts the E partials
                 asm volatile(
                     "v_add_f32 %0, %8, %0\n\t"
                     "v_max_f32 %2, %3, %7\n\t"
@@ -375,12 +409,31 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         if constexpr ((EXP & 4) && (c & 1)) {  // 4 accumulators: half-length E dependency chains
             rc.p2 = fmaxf(fmaxf(rc.p2, st.M[k + 3]), st.M[k + 2]);
             rc.p3 = fmaxf(fmaxf(rc.p3, st.M[k + 1]), st.M[k]);
-        } else if constexpr (c == C4 - 1 && !(EXP & 4)) {  // first chunk of the row: no -inf seed
+        } else if constexpr (!SPLIT && c == CA - 1 && !(EXP & 4)) {  // the row's first chunk: no -inf seed
             rc.p0 = fmaxf(st.M[k + 3], st.M[k + 2]);
             rc.p1 = fmaxf(st.M[k + 1], st.M[k]);
         } else {
             rc.p0 = fmaxf(fmaxf(rc.p0, st.M[k + 3]), st.M[k + 2]);
             rc.p1 = fmaxf(fmaxf(rc.p1, st.M[k + 1]), st.M[k]);
+        }
+    };
+    // SPLIT: one B half (states SA + 2h + 1, + 2 of the lane), emissions already in registers;
+    // processed before the A chunks (higher states first), the first one seeds the E partials.
+    auto bhalf = [&](St& st, auto& rc, auto hh) {
+        constexpr int h = decltype(hh)::value;
+        constexpr int k = SA + 2 * h;
+        const float2 ev = bring.v[h];
+        st.M[k + 1] = ev.y + fmaxf(st.M[k], rc.Bt);
+        st.M[k] = ev.x + fmaxf(h == 0 ? rc.nbrB : st.M[k - 1], rc.Bt);
+        if constexpr (h == HB - 1) {
+            rc.p0 = fmaxf(st.M[k + 1], st.M[k]);
+            if constexpr (HB == 1) rc.p1 = NINF;
+        } else if constexpr (h == HB - 2) {
+            rc.p1 = fmaxf(st.M[k + 1], st.M[k]);
+        } else if constexpr ((HB - 1 - h) & 1) {
+            rc.p1 = fmaxf(fmaxf(rc.p1, st.M[k + 1]), st.M[k]);
+        } else {
+            rc.p0 = fmaxf(fmaxf(rc.p0, st.M[k + 1]), st.M[k]);
         }
     };
     // Row epilogue: E over the group, the specials (MSV_HMM.cpp:107-110), cursor advance.
@@ -441,15 +494,25 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
 
     RowCtx<PF> xr;  // XROW: the ring persists across rows
     if constexpr (XROW) fill_ring(xr, row_ptr(s0));
+    fill_b(s0.r[0]);
 
     // All chunks of one row, C4-1 .. 0, each step pinned so only the rings' registers are live.
     auto row = [&](St& st, auto& rc, const float4* ep) {
         prologue(st, rc, ep);
+        if constexpr (SPLIT) {
+            [&]<int... I>(std::integer_sequence<int, I...>) {
+                ((bhalf(st, rc, std::integral_constant<int, HB - 1 - I>{}),
+                  [&] { if constexpr (I & 1) __builtin_amdgcn_sched_barrier(0); }()),
+                 ...);
+            }(std::make_integer_sequence<int, HB>{});
+            fill_b(st.r[1]);  // this row's B halves are consumed: request the next row's
+            __builtin_amdgcn_sched_barrier(0);
+        }
         [&]<int... I>(std::integer_sequence<int, I...>) {
-            ((chunk(st, rc, std::integral_constant<int, C4 - 1 - I>{}),
+            ((chunk(st, rc, std::integral_constant<int, CA - 1 - I>{}),
               [&] { if constexpr (!(EXP & 2) || (I & 1)) __builtin_amdgcn_sched_barrier(0); }()),
              ...);
-        }(std::make_integer_sequence<int, C4>{});
+        }(std::make_integer_sequence<int, CA>{});
         epilogue(st, rc);
     };
 
@@ -521,6 +584,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             if (s0.pos == s0.endp) {
                 finish(s0);
                 if constexpr (XROW) fill_ring(xr, row_ptr(s0));
+                fill_b(s0.r[0]);
             }
             if constexpr (D == 2) {
                 if (s1.pos == s1.endp) finish(s1);
@@ -671,8 +735,14 @@ hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t
 #define MSV_EXPERIMENT(G_, S_, W_, P_, D_, X_)                                                            \
     Variant{G_, S_, W_, P_, D_, lds_rows_for(G_, S_), lds_rows_for(G_, S_) < kTableRows,                  \
             reinterpret_cast<const void*>(                                                                 \
-                &msv_batch_kernel<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_, X_>),           \
+                &msv_batch_kernel<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_, 0, X_>),        \
             "exp" #X_ "_g" #G_ "_s" #S_ "_w" #W_ "_p" #P_ "_d" #D_}
+
+// Split layout (one sequence per wave): SA states per lane from LDS (20 rows), S - SA from L2.
+#define MSV_SPLIT_VARIANT(S_, SA_, W_, P_)                                                                \
+    Variant{64, S_, W_, P_, 1, kAminoAcids, false,                                                        \
+            reinterpret_cast<const void*>(&msv_batch_kernel<64, S_, W_, P_, false, 1, SA_>),               \
+            "msv_g64_s" #S_ "_a" #SA_ "_w" #W_ "_p" #P_ "_d1", SA_}
 
 static const Variant kVariants[] = {
 #include "msv_variants.inc"
