@@ -86,11 +86,12 @@ msv_status hip_status(hipError_t e) {
 // specials/reduction, times the lanes a sequence occupies.  A BIG table costs little with one
 // sequence per wave (G = 64: wave-uniform LDS/L2 row split) and a lot with 2-4 sequences per wave
 // (generic loads with per-lane address selects); measured on 2405.hmm: 7.4 vs 10.5 ms.
-// A split table (one sequence per wave, the lane's last S - SA states read from L2 every row) costs
-// two more DPP moves per row and no class branch.
+// A split table (the lane's last S - SA states read from L2 every row) costs the B-table address and
+// loads per row and no class branch, so it also runs two sequences per wave (G = 32).
 double variant_cost(const msvk::Variant& v) {
     const double big = !v.big ? 1.0 : (v.G == 64 ? 1.03 : 1.6);
-    const double row = v.G == 64 ? (v.sa ? 38.0 : 36.0) : 26.0;  // + permlane32 step, scalar bookkeeping
+    // G = 64: + permlane32 step, scalar bookkeeping
+    const double row = (v.G == 64 ? 36.0 : 26.0) + (v.sa ? 2.0 : 0.0);
     return (2.5 * v.S + row) * v.G * big * (v.pf == 2 ? 1.0 : 1.05) * (v.streams == 2 ? 1.15 : 1.0);
 }
 
@@ -169,9 +170,9 @@ struct msv_profile {
 // Lays the MSV table out for variant v and uploads it:
 // [row r][chunk c][lane gl] float4 = e[r][gl*S + 4c + 1 .. +4]; states beyond LENG are -inf
 // (never win a max); row 20 is the +inf poison row for codes >= 20.
-// Split variants (v->sa > 0, G = 64): an A table [20 rows][SA/4][G] float4 (lane gl's states gl*SA + 1 ..,
-// staged in LDS) followed by a B table [21 rows][(S-SA)/2][G] float2 (lane gl's states
-// 64*SA + gl*(S-SA) + 1 .., read from L2; row 20 = poison).
+// Split variants (v->sa > 0, G = 32/64, lane gl owns states gl*S + 1 .. gl*S + S as usual): an A table
+// [20 rows][SA/4][G] float4 (the lane's first SA states, staged in LDS) followed by a B table
+// [21 rows][(S-SA)/2][G] float2 (its last S - SA states, read from L2; row 20 = poison).
 static msv_status install_plan(msv_profile* p, const msvk::Variant* v, Plan& plan) {
     const uint32_t model_length = p->model_length, R = model_length - 1;
     const int G = v->G, S = v->S, C4 = S / 4;
@@ -193,8 +194,8 @@ static msv_status install_plan(msv_profile* p, const msvk::Variant* v, Plan& pla
                     }
     };
     if (v->sa > 0) {
-        block(msvk::kAminoAcids, v->sa / 4, 1, v->sa, 4);
-        block(msvk::kTableRows, (S - v->sa) / 2, static_cast<uint32_t>(G * v->sa + 1), S - v->sa, 2);
+        block(msvk::kAminoAcids, v->sa / 4, 1, S, 4);
+        block(msvk::kTableRows, (S - v->sa) / 2, static_cast<uint32_t>(v->sa + 1), S, 2);
     } else {
         block(msvk::kTableRows, C4, 1, S, 4);
     }

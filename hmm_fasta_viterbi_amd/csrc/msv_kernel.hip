@@ -61,8 +61,6 @@ constexpr int DPP_ROW_SHR1 = 0x111;    // row_shr:1
 constexpr int DPP_ROW_MIRROR = 0x140;  // row_mirror
 constexpr int DPP_ROW_HMIRROR = 0x141; // row_half_mirror
 constexpr int DPP_ROW_BCAST15 = 0x142; // row_bcast:15
-constexpr int DPP_WAVE_SHR1 = 0x138;   // wave_shr:1
-constexpr int DPP_WAVE_ROR1 = 0x13C;   // wave_ror:1
 
 // M_{j-1} for the first state of each lane: the last state of the previous lane of the same
 // group; -inf (the dummy M0 column, MSV_HMM.cpp:86) for the first lane of a group.  `old` supplies
@@ -168,15 +166,16 @@ template <int PF>
 struct RowCtx {
     static constexpr int kPF = PF;
     const float4* ep;
-    float Bt, nbr, nbrB, p0, p1, p2, p3;  // nbrB: split layout, neighbour of the lane's first B state
+    float Bt, nbr, p0, p1, p2, p3;
     uint32_t rnext;  // residue code RPF rows ahead
     float4 ring[PF];
 };
 
-// SA > 0 selects the SPLIT layout (one sequence per wave, G = 64): each lane's first SA states (the
-// "A block", states 1..64*SA) have all 20 residue rows in LDS, its last S - SA states (the "B block",
-// states 64*SA+1..) are read from the global table (L2) for every row -- no per-row LDS/L2 class
-// branch; the next row's B chunks are requested one row ahead.
+// SA > 0 selects the SPLIT layout (G = 32 or 64, tables too large for LDS): lane gl still owns the S
+// consecutive states gl*S+1 .. gl*S+S; its first SA states (the "A block") have all 20 residue rows in
+// LDS, its last S - SA states (the "B block") are read from the global table (L2) for every row -- no
+// per-row LDS/L2 class branch, so the groups of a wave run the same row body whatever their residues;
+// the next row's B halves are requested one row ahead.
 template <int G, int S, int WAVES, int PF, bool BIG, int D, int SA = 0, int EXP = 0>
 __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs a) {
     constexpr bool SPLIT = SA > 0;
@@ -185,7 +184,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     using St = Stream<S, (EXP & 64) ? 1 : ((SPLIT && residue_prefetch<S>() < 2) ? 2 : residue_prefetch<S>())>;
     static_assert(SPLIT ? (S - SA) % 2 == 0 : S % 4 == 0, "float4 chunks (A block), float2 halves (B block)");
     static_assert(PF >= 1 && D >= 1 && D <= 2, "PF >= 1, D in {1, 2}");
-    static_assert(!SPLIT || (G == 64 && !BIG && D == 1 && SA % 4 == 0 && SA < S), "split: one sequence per wave");
+    static_assert(!SPLIT || (G >= 32 && !BIG && D == 1 && SA % 4 == 0 && SA < S), "split: 32/64-lane groups");
     constexpr int C4 = S / 4;
     constexpr int CA = SPLIT ? SA / 4 : C4;  // float4 chunks per lane whose emissions are staged in LDS
     constexpr int HB = SPLIT ? (S - SA) / 2 : 0;  // SPLIT: float2 halves per lane read from the B table
@@ -319,13 +318,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         }
         rc.ep = ep;
         rc.Bt = st.B + trBMk;
-        if constexpr (SPLIT) {
-            // A block: lane l-1's last A state (-inf for lane 0); B block: lane l-1's last B state,
-            // and for lane 0 the last A state of lane 63 (wave_ror:1, then wave_shr:1 keeps it there)
-            st.nbr = shift_in<G>(st.M[SA - 1], st.nbr);
-            rc.nbr = st.nbr;
-            rc.nbrB = dpp<DPP_WAVE_SHR1>(dpp_perm<DPP_WAVE_ROR1>(st.M[SA - 1]), st.M[S - 1]);
-        } else if constexpr (G >= 16) {
+        if constexpr (G >= 16) {
             st.nbr = shift_in<G>(st.M[S - 1], st.nbr);
             rc.nbr = st.nbr;
         } else {
@@ -418,13 +411,14 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         }
     };
     // SPLIT: one B half (states SA + 2h + 1, + 2 of the lane), emissions already in registers;
-    // processed before the A chunks (higher states first), the first one seeds the E partials.
+    // processed before the A chunks (higher states first, so M[SA - 1] is still the previous row's),
+    // the first one seeds the E partials.
     auto bhalf = [&](St& st, auto& rc, auto hh) {
         constexpr int h = decltype(hh)::value;
         constexpr int k = SA + 2 * h;
         const float2 ev = bring.v[h];
         st.M[k + 1] = ev.y + fmaxf(st.M[k], rc.Bt);
-        st.M[k] = ev.x + fmaxf(h == 0 ? rc.nbrB : st.M[k - 1], rc.Bt);
+        st.M[k] = ev.x + fmaxf(st.M[k - 1], rc.Bt);
         if constexpr (h == HB - 1) {
             rc.p0 = fmaxf(st.M[k + 1], st.M[k]);
             if constexpr (HB == 1) rc.p1 = NINF;
@@ -454,7 +448,11 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         // reduction across lanes (DPP butterfly) leaves the row's dependency chain.
         // (G = 64: a row_bcast:15/31 + v_readlane reduction to an SGPR measured 13% slower on
         // 2405.hmm than the permlane swaps -- the SGPR round trip stalls the row)
-        if (__builtin_expect(__any(st.J >= st.N), 0)) {
+        // (EXP & 4096: timing-only, B = N + move on every row with no test -- right only while no
+        // J_l reaches N, i.e. on random-like sequences: the cost of the per-row test and branch)
+        if constexpr (EXP & 4096) {
+            st.B = st.N + st.move;
+        } else if (__builtin_expect(__any(st.J >= st.N), 0)) {
             st.B = fmaxf(st.N, group_max<G>(st.J)) + st.move;
         } else {
             st.B = st.N + st.move;
@@ -738,11 +736,11 @@ hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t
                 &msv_batch_kernel<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_, 0, X_>),        \
             "exp" #X_ "_g" #G_ "_s" #S_ "_w" #W_ "_p" #P_ "_d" #D_}
 
-// Split layout (one sequence per wave): SA states per lane from LDS (20 rows), S - SA from L2.
-#define MSV_SPLIT_VARIANT(S_, SA_, W_, P_)                                                                \
-    Variant{64, S_, W_, P_, 1, kAminoAcids, false,                                                        \
-            reinterpret_cast<const void*>(&msv_batch_kernel<64, S_, W_, P_, false, 1, SA_>),               \
-            "msv_g64_s" #S_ "_a" #SA_ "_w" #W_ "_p" #P_ "_d1", SA_}
+// Split layout (G = 32 or 64): SA states per lane from LDS (20 rows), S - SA from L2.
+#define MSV_SPLIT_VARIANT(G_, S_, SA_, W_, P_)                                                            \
+    Variant{G_, S_, W_, P_, 1, kAminoAcids, false,                                                        \
+            reinterpret_cast<const void*>(&msv_batch_kernel<G_, S_, W_, P_, false, 1, SA_>),               \
+            "msv_g" #G_ "_s" #S_ "_a" #SA_ "_w" #W_ "_p" #P_ "_d1", SA_}
 
 static const Variant kVariants[] = {
 #include "msv_variants.inc"
@@ -760,6 +758,8 @@ static const Variant kVariants[] = {
     MSV_EXPERIMENT(16, 8, 16, 2, 1, 32),
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 32),
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 2048),
+    MSV_EXPERIMENT(16, 8, 4, 2, 1, 4096),
+    MSV_EXPERIMENT(16, 88, 16, 2, 1, 4096),
 #endif
 };
 

@@ -107,6 +107,27 @@ def test_bad_residue_raises_like_reference():
     assert np.isfinite(e.run_on_sequence("#ACDEF"))
 
 
+def test_bad_residue_every_large_table_layout():
+    """Codes >= 20 must reach the +inf poison row in every layout of a table larger than LDS: the
+    split layouts (LDS rows 0..19 only, poison row in the global B table; G = 32 and 64) and the
+    G = 64 LDS/L2 row-class layout."""
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("2405.hmm")))
+    good_c, good_o = random_batch(31, 40, 1, 300)
+    bad = good_c.copy()
+    bad[int(good_o[17]) + 3] = 20
+    want = OracleProfile("2405").score_batch(good_c, good_o)
+    names = [v for v in msv.MSV_HMM.variants()
+             if not v.startswith("exp") and _variant_shape(v)[0] * _variant_shape(v)[1] >= 2405
+             and _variant_shape(v)[0] >= 32]
+    assert any("_a" in v and v.startswith("msv_g32") for v in names)
+    for name in names:
+        e.set_variant(name)
+        with pytest.raises(IndexError):
+            e.score_batch(codes=bad, offsets=good_o)
+        assert np.array_equal(bits(e.score_batch(codes=good_c, offsets=good_o)), bits(want)), name
+    e.close()
+
+
 def test_long_sequence_grows_table():
     e = engine("100.hmm")
     codes, offsets = random_batch(77, 2, 140000, 150000)
