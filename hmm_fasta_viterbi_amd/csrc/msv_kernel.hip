@@ -450,12 +450,11 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         // 2405.hmm than the permlane swaps -- the SGPR round trip stalls the row)
         // (EXP & 4096: timing-only, B = N + move on every row with no test -- right only while no
         // J_l reaches N, i.e. on random-like sequences: the cost of the per-row test and branch)
-        if constexpr (EXP & 4096) {
-            st.B = st.N + st.move;
-        } else if (__builtin_expect(__any(st.J >= st.N), 0)) {
-            st.B = fmaxf(st.N, group_max<G>(st.J)) + st.move;
-        } else {
-            st.B = st.N + st.move;
+        // The common value first and the rare one as an overwrite, so the common path falls through
+        // (as an if/else the else-block was laid out of line: two taken branches per row).
+        st.B = st.N + st.move;
+        if constexpr (!(EXP & 4096)) {
+            if (__builtin_expect(__any(st.J >= st.N), 0)) st.B = fmaxf(st.N, group_max<G>(st.J)) + st.move;
         }
         ++st.pos;
 #pragma unroll
