@@ -156,7 +156,8 @@ struct Stream {
     // pos: residue of the current row; endpos: last residue (prefetch clamp); endp: pos after the
     // last row; ev: pos at which the next event fires (the half-way index fetch, then endp)
     uint32_t pos, endpos, endp, ev, seq;
-    uint32_t r[RPF];  // residue codes of the next RPF rows (r[0] = this row)
+    uint8_t r[RPF];   // residue codes of the next RPF rows (bytes: a 32-bit slot made the compiler
+                      // zero-extend each load where it lands, i.e. wait for it in the same row)
     bool active;
     bool junk;        // current "sequence" is an empty/too-long record: discard its row
 };
@@ -167,7 +168,7 @@ struct RowCtx {
     static constexpr int kPF = PF;
     const float4* ep;
     float Bt, nbr, p0, p1, p2, p3;
-    uint32_t rnext;  // residue code RPF rows ahead
+    uint8_t rnext;   // residue code RPF rows ahead
     float4 ring[PF];
 };
 
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // Cross-row emission prefetch: when the ring holds a whole row (small profiles), the NEXT row's
     // chunks are requested right after this row's last cell update, so the LDS latency hides behind
     // the E butterfly and the specials instead of stalling the start of every row.
-    constexpr bool XROW = !BIG && !SPLIT && D == 1 && PF >= C4 && residue_prefetch<S>() >= 2;
+    constexpr bool XROW = !BIG && !SPLIT && D == 1 && PF >= C4 && St::RPF >= 2;
     static_assert(SPLIT || BIG == (LDS_ROWS < kTableRows), "BIG <=> table does not fit LDS");
     __shared__ float4 tab[LDS_ROWS * ROW_F4];
 
@@ -219,8 +220,19 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     constexpr uint32_t kNone = 0xFFFFFFFFu;
     uint32_t pending = kNone;
 
-    // Start the next non-empty sequence in a stream (or retire the stream).
-    auto begin = [&](St& st) {
+    // Residue slots rotate instead of shifting (ROT): the row of phase P reads its residue from
+    // r[P] and loads the residue RPF rows ahead into the same slot, and the main loop is unrolled
+    // over the RPF phases.  A shift register moves every prefetched byte once per row, and a move of
+    // a register with a load in flight waits for that load (s_waitcnt vmcnt(0) in every row): the
+    // short rows of small profiles then last as long as one L2 round trip.  Paths that keep the
+    // shift: one residue of prefetch (nothing to shift), the G = 64 row-class layout and D = 2.
+    constexpr bool ROT = !BIG && D == 1 && St::RPF > 1;
+    using Ph0 = std::integral_constant<int, 0>;
+
+    // Start the next non-empty sequence in a stream (or retire the stream); `ph` is the phase of the
+    // row that will run next (its residue goes to slot r[ph]).
+    auto begin = [&](St& st, auto ph) {
+        constexpr int PH = decltype(ph)::value;
         // Loop-free on purpose: a retry loop around the group broadcast here was unswitched by
         // the compiler into per-lane copies (see group_take).  An empty (or too long) record
         // instead becomes a one-row "junk" stream: its score is written now, one row is computed
@@ -266,11 +278,11 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         st.active = !retire;
         st.junk = !run;
 #pragma unroll
-        for (int q = 0; q < St::RPF; ++q) st.r[q] = res[min(st.pos + q, st.endpos)];
+        for (int q = 0; q < St::RPF; ++q) st.r[(PH + q) % St::RPF] = res[min(st.pos + q, st.endpos)];
     };
     auto init = [&](St& st) {
         st.nbr = NINF;
-        begin(st);
+        begin(st, Ph0{});
     };
     // Row prologue: next residue prefetch, emission row pointer, Bt, the j-1 neighbour, ring fill.
     // LDS row of residue code r for this lane (codes >= 20 -> the poison row).  (A hand-written
@@ -295,9 +307,9 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             for (int q = 0; q < HB; ++q) bring.v[q] = bp[q * G];
         }
     };
-    auto row_ptr = [&](St& st) -> const float4* {
+    auto row_ptr = [&](St& st, auto ph) -> const float4* {
         if constexpr (!BIG) {
-            return lds_row(st.r[0]);
+            return lds_row(st.r[decltype(ph)::value]);
         } else {
             const uint32_t rr = min(st.r[0], static_cast<uint32_t>(kPoisonRow));
             return (rr < static_cast<uint32_t>(LDS_ROWS)) ? &tab[rr * ROW_F4 + gl] : &a.etab[rr * ROW_F4 + gl];
@@ -309,10 +321,12 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
 #pragma unroll
         for (int q = 0; q < (P < CA ? P : CA); ++q) rc.ring[q] = ep[(CA - 1 - q) * G];
     };
-    auto prologue = [&](St& st, auto& rc, const float4* ep) {
+    auto prologue = [&](St& st, auto& rc, const float4* ep, auto ph) {
         // (EXP & 32: timing-only, synthetic residues instead of the stream -> wrong scores)
         if constexpr (EXP & 32) {
             rc.rnext = (st.pos * 7u) % 20u;
+        } else if constexpr (EXP & 8192) {  // timing-only: no residue load, no arithmetic either
+            rc.rnext = st.r[(decltype(ph)::value + St::RPF - 1) % St::RPF] ^ 1u;
         } else {
             rc.rnext = res[min(st.pos + St::RPF, st.endpos)];
         }
@@ -431,14 +445,14 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         }
     };
     // Row epilogue: E over the group, the specials (MSV_HMM.cpp:107-110), cursor advance.
-    auto epilogue = [&](St& st, auto& rc) {
+    auto epilogue = [&](St& st, auto& rc, auto ph) {
         const float Elane = (EXP & 4) ? fmaxf(fmaxf(rc.p0, rc.p1), fmaxf(rc.p2, rc.p3)) : fmaxf(rc.p0, rc.p1);
         // Per-lane partials (see Stream): J_l, and C_l unless C == J (tr_E_C == tr_E_J, which is
         // always the case for the reference's nu = 2, MSV_HMM.cpp:49-53: then the C and J
         // recurrences are identical and C is read from J at the end).
         const float EJ = Elane + tEJ;
         st.J = fmaxf(st.J + st.loop, EJ);
-        if (!sameEJ) {
+        if (__builtin_expect(!sameEJ, 0)) {
             st.C = fmaxf(st.C + st.loop, Elane + tEC);
             asm volatile("" ::: "memory");  // keep a real (scalar) branch, not a per-row select
         }
@@ -457,11 +471,16 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             if (__builtin_expect(__any(st.J >= st.N), 0)) st.B = fmaxf(st.N, group_max<G>(st.J)) + st.move;
         }
         ++st.pos;
+        if constexpr (ROT) {
+            st.r[decltype(ph)::value] = rc.rnext;  // this row's slot now holds the row RPF ahead
+        } else {
 #pragma unroll
-        for (int q = 0; q + 1 < St::RPF; ++q) st.r[q] = st.r[q + 1];
-        st.r[St::RPF - 1] = rc.rnext;
+            for (int q = 0; q + 1 < St::RPF; ++q) st.r[q] = st.r[q + 1];
+            st.r[St::RPF - 1] = rc.rnext;
+        }
     };
-    auto finish = [&](St& st) {
+    // `ph`: phase of the row that runs next.
+    auto finish = [&](St& st, auto ph) {
         // Every lane of the group is here (pos == endp is group-uniform), so the group reduction of
         // the C partials reads only active lanes of the same group.
         // (the copy of J is opaque so the compiler cannot hoist this select into every row)
@@ -473,7 +492,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             a.scores[st.seq] = sc;
             if (!(sc <= 3.402823466e38f)) atomicOr(a.errors, kErrBadResidue);  // poison row hit
         }
-        begin(st);
+        begin(st, ph);
     };
 
     // D independent sequences per lane group ("streams"): their rows interleave chunk by chunk,
@@ -490,19 +509,22 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // the LDS-row class for G = 64 -- measured no gain, and 15% LOSS for the latter on 2405.hmm.)
 
     RowCtx<PF> xr;  // XROW: the ring persists across rows
-    if constexpr (XROW) fill_ring(xr, row_ptr(s0));
+    if constexpr (XROW) fill_ring(xr, row_ptr(s0, Ph0{}));
     fill_b(s0.r[0]);
 
+    // slot of the residue of the row after a row of phase P
+    auto next_slot = [](auto ph) { return (decltype(ph)::value + 1) % St::RPF; };
+
     // All chunks of one row, C4-1 .. 0, each step pinned so only the rings' registers are live.
-    auto row = [&](St& st, auto& rc, const float4* ep) {
-        prologue(st, rc, ep);
+    auto row = [&](St& st, auto& rc, const float4* ep, auto ph) {
+        prologue(st, rc, ep, ph);
         if constexpr (SPLIT) {
             [&]<int... I>(std::integer_sequence<int, I...>) {
                 ((bhalf(st, rc, std::integral_constant<int, HB - 1 - I>{}),
                   [&] { if constexpr (I & 1) __builtin_amdgcn_sched_barrier(0); }()),
                  ...);
             }(std::make_integer_sequence<int, HB>{});
-            fill_b(st.r[1]);  // this row's B halves are consumed: request the next row's
+            fill_b(st.r[next_slot(ph)]);  // this row's B halves are consumed: request the next row's
             __builtin_amdgcn_sched_barrier(0);
         }
         [&]<int... I>(std::integer_sequence<int, I...>) {
@@ -510,85 +532,120 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
               [&] { if constexpr (!(EXP & 2) || (I & 1)) __builtin_amdgcn_sched_barrier(0); }()),
              ...);
         }(std::make_integer_sequence<int, CA>{});
-        epilogue(st, rc);
+        epilogue(st, rc, ph);
     };
 
     // Wave-uniform loop condition, refreshed only when a stream finishes.
     bool live = __any(D == 2 ? (s0.active || s1.active) : s0.active);
-    while (live) {
-        if constexpr (BIG && G == 64 && (EXP & 256)) {
-            // (timing-only: vector row index, all rows from LDS, no readfirstlane -> wrong scores)
-            RowCtx<PF> c0;
-            row(s0, c0, &tab[(min(s0.r[0], static_cast<uint32_t>(kPoisonRow)) % LDS_ROWS) * ROW_F4 + gl]);
-        } else if constexpr (BIG && G == 64) {
-            // One sequence per wave: the residue, hence the table row's home, is wave-uniform, so
-            // the LDS rows and the L2 rows run as two separate (scalar-branched) row bodies with
-            // precise waits -- no generic loads, no per-lane selects.  An L2 row requests up to 10
-            // chunks up front to pay the L2 latency about once per row.
-            // (a vector compare with exec masking instead of readfirstlane measured 1.5% slower;
-            // reading the class one row early into an SGPR changed nothing; without the class branch
-            // at all -- EXP & 256, wrong scores -- the row is 10% faster)
-            const uint32_t rr =
-                __builtin_amdgcn_readfirstlane(min(s0.r[0], static_cast<uint32_t>(kPoisonRow)));
-            // (EXP & 8: timing-only, every row served from LDS -> wrong scores; EXP & 16: L2 rows
-            // with the LDS ring depth)
-            if ((EXP & 8) || rr < static_cast<uint32_t>(LDS_ROWS)) {
-                RowCtx<PF> c0;
-                row(s0, c0, &tab[((EXP & 8) ? rr % LDS_ROWS : rr) * ROW_F4 + gl]);
-            } else {
-                RowCtx<(EXP & 16) ? PF : (C4 < 10 ? C4 : 10)> c0;
-                row(s0, c0, &a.etab[rr * ROW_F4 + gl]);
-            }
-        } else if constexpr (XROW) {
-            prologue(s0, xr, nullptr);
+
+    // One row of phase P of the single-stream, non-row-class paths (XROW or plain), then its events.
+    // Returns whether the wave still has work.
+    auto step = [&](auto ph) -> bool {
+        constexpr int PN = (decltype(ph)::value + 1) % St::RPF;
+        using PhN = std::integral_constant<int, PN>;
+        if constexpr (XROW) {
+            prologue(s0, xr, nullptr, ph);
             [&]<int... I>(std::integer_sequence<int, I...>) {
                 ((chunk(s0, xr, std::integral_constant<int, C4 - 1 - I>{})), ...);
             }(std::make_integer_sequence<int, C4>{});
-            // s0.r[1] is the residue of the next row (discarded if this row ends the sequence)
-            fill_ring(xr, lds_row(s0.r[1]));
-            epilogue(s0, xr);
-        } else if constexpr (D == 1) {
-            RowCtx<PF> c0;
-            row(s0, c0, row_ptr(s0));
+            // r[PN] is the residue of the next row (discarded if this row ends the sequence)
+            fill_ring(xr, lds_row(s0.r[PN]));
+            epilogue(s0, xr, ph);
         } else {
-            RowCtx<PF> c0, c1;
-            prologue(s0, c0, row_ptr(s0));
-            prologue(s1, c1, row_ptr(s1));
-            [&]<int... I>(std::integer_sequence<int, I...>) {
-                ((chunk(s0, c0, std::integral_constant<int, C4 - 1 - I>{}),
-                  chunk(s1, c1, std::integral_constant<int, C4 - 1 - I>{}),
-                  [&] { if constexpr (!(EXP & 2) || (I & 1)) __builtin_amdgcn_sched_barrier(0); }()),
-                 ...);
-            }(std::make_integer_sequence<int, C4>{});
-            epilogue(s0, c0);
-            epilogue(s1, c1);
+            RowCtx<PF> c0;
+            row(s0, c0, row_ptr(s0, ph), ph);
         }
-        // Events (one compare per stream and row; the handling is rare and wave-uniformly skipped):
-        // the half-way fetch of the next index, then the end of the sequence.  (G = 64: the cursor
-        // is wave-uniform and the compares are scalar; there the guard made the compiler copy the
-        // whole DP row at the loop latch, +12% per row on 2405.hmm, so it is left out.)
-        if (G == 64 || __any(D == 2 ? (s0.pos == s0.ev || s1.pos == s1.ev) : s0.pos == s0.ev)) {
+        // Events: see the generic loop below.
+        if (G == 64 || __any(s0.pos == s0.ev)) {
             if (s0.pos == s0.ev && s0.ev != s0.endp) {
                 if (pending == kNone) pending = group_take<G>(a.counter, leader, lane);
                 s0.ev = s0.endp;
             }
-            if constexpr (D == 2) {
-                if (s1.pos == s1.ev && s1.ev != s1.endp) {
-                    if (pending == kNone) pending = group_take<G>(a.counter, leader, lane);
-                    s1.ev = s1.endp;
-                }
-            }
             if (s0.pos == s0.endp) {
-                finish(s0);
-                if constexpr (XROW) fill_ring(xr, row_ptr(s0));
-                fill_b(s0.r[0]);
+                finish(s0, PhN{});
+                if constexpr (XROW) fill_ring(xr, row_ptr(s0, PhN{}));
+                fill_b(s0.r[PN]);
             }
-            if constexpr (D == 2) {
-                if (s1.pos == s1.endp) finish(s1);
-            }
-            live = __any(D == 2 ? (s0.active || s1.active) : s0.active);
+            live = __any(s0.active);
         }
         ++rows_done;
+        return live;
+    };
+
+    while (live) {
+        if constexpr (ROT) {
+            // RPF rows per iteration, one per residue slot; stops after any row that retires the wave
+            [&]<int... I>(std::integer_sequence<int, I...>) {
+                (void)(step(std::integral_constant<int, I>{}) && ...);
+            }(std::make_integer_sequence<int, St::RPF>{});
+        } else {
+            if constexpr (BIG && G == 64 && (EXP & 256)) {
+                // (timing-only: vector row index, all rows from LDS, no readfirstlane -> wrong scores)
+                RowCtx<PF> c0;
+                row(s0, c0, &tab[(min(s0.r[0], static_cast<uint32_t>(kPoisonRow)) % LDS_ROWS) * ROW_F4 + gl],
+                    Ph0{});
+            } else if constexpr (BIG && G == 64) {
+                // One sequence per wave: the residue, hence the table row's home, is wave-uniform, so
+                // the LDS rows and the L2 rows run as two separate (scalar-branched) row bodies with
+                // precise waits -- no generic loads, no per-lane selects.  An L2 row requests up to 10
+                // chunks up front to pay the L2 latency about once per row.
+                // (a vector compare with exec masking instead of readfirstlane measured 1.5% slower;
+                // reading the class one row early into an SGPR changed nothing; without the class
+                // branch at all -- EXP & 256, wrong scores -- the row is 10% faster)
+                const uint32_t rr =
+                    __builtin_amdgcn_readfirstlane(min(s0.r[0], static_cast<uint32_t>(kPoisonRow)));
+                // (EXP & 8: timing-only, every row served from LDS -> wrong scores; EXP & 16: L2 rows
+                // with the LDS ring depth)
+                if ((EXP & 8) || rr < static_cast<uint32_t>(LDS_ROWS)) {
+                    RowCtx<PF> c0;
+                    row(s0, c0, &tab[((EXP & 8) ? rr % LDS_ROWS : rr) * ROW_F4 + gl], Ph0{});
+                } else {
+                    RowCtx<(EXP & 16) ? PF : (C4 < 10 ? C4 : 10)> c0;
+                    row(s0, c0, &a.etab[rr * ROW_F4 + gl], Ph0{});
+                }
+            } else if constexpr (D == 1) {
+                RowCtx<PF> c0;
+                row(s0, c0, row_ptr(s0, Ph0{}), Ph0{});
+            } else {
+                RowCtx<PF> c0, c1;
+                prologue(s0, c0, row_ptr(s0, Ph0{}), Ph0{});
+                prologue(s1, c1, row_ptr(s1, Ph0{}), Ph0{});
+                [&]<int... I>(std::integer_sequence<int, I...>) {
+                    ((chunk(s0, c0, std::integral_constant<int, C4 - 1 - I>{}),
+                      chunk(s1, c1, std::integral_constant<int, C4 - 1 - I>{}),
+                      [&] { if constexpr (!(EXP & 2) || (I & 1)) __builtin_amdgcn_sched_barrier(0); }()),
+                     ...);
+                }(std::make_integer_sequence<int, C4>{});
+                epilogue(s0, c0, Ph0{});
+                epilogue(s1, c1, Ph0{});
+            }
+            // Events (one compare per stream and row; the handling is rare and wave-uniformly
+            // skipped): the half-way fetch of the next index, then the end of the sequence.  (G = 64:
+            // the cursor is wave-uniform and the compares are scalar; there the guard made the
+            // compiler copy the whole DP row at the loop latch, +12% per row on 2405.hmm, so it is
+            // left out.)
+            if (G == 64 || __any(D == 2 ? (s0.pos == s0.ev || s1.pos == s1.ev) : s0.pos == s0.ev)) {
+                if (s0.pos == s0.ev && s0.ev != s0.endp) {
+                    if (pending == kNone) pending = group_take<G>(a.counter, leader, lane);
+                    s0.ev = s0.endp;
+                }
+                if constexpr (D == 2) {
+                    if (s1.pos == s1.ev && s1.ev != s1.endp) {
+                        if (pending == kNone) pending = group_take<G>(a.counter, leader, lane);
+                        s1.ev = s1.endp;
+                    }
+                }
+                if (s0.pos == s0.endp) {
+                    finish(s0, Ph0{});
+                    fill_b(s0.r[0]);
+                }
+                if constexpr (D == 2) {
+                    if (s1.pos == s1.endp) finish(s1, Ph0{});
+                }
+                live = __any(D == 2 ? (s0.active || s1.active) : s0.active);
+            }
+            ++rows_done;
+        }
     }
     // Self-resetting dequeue counter: the last wave of the grid to leave puts counter[0] (next
     // index) and counter[1] (waves left) back to 0, so the next launch needs no memset.  Every
@@ -758,6 +815,8 @@ static const Variant kVariants[] = {
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 32),
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 2048),
     MSV_EXPERIMENT(16, 8, 4, 2, 1, 4096),
+    MSV_EXPERIMENT(16, 8, 4, 2, 1, 8192),
+    MSV_EXPERIMENT(64, 24, 16, 6, 1, 8192),
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 4096),
 #endif
 };
