@@ -257,6 +257,23 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             atomicOr(a.errors, kErrTooLong);
         }
         const bool run = !retire && !empty && !too_long;
+        if constexpr ((EXP & 16384) != 0) {
+            // Tail priority: the groups that dequeue the last indices hold the most remaining rows
+            // when the queue drains, so their waves get VALU issue priority over older waves
+            // (arbitration is priority, then age): 1 / 2 / 3 for the last K, K/2, K/4 indices,
+            // K = groups in flight.  Priority only rises, since indices rise.
+            const uint32_t K = gridDim.x * WAVES * (64 / G) * ((EXP & 32768) ? 2u : 1u);
+            const uint32_t n = a.n;
+            if (n > K) {
+                if (__any(run && idx >= n - K / 4)) {
+                    __builtin_amdgcn_s_setprio(3);
+                } else if (__any(run && idx >= n - K / 2)) {
+                    __builtin_amdgcn_s_setprio(2);
+                } else if (__any(run && idx >= n - K)) {
+                    __builtin_amdgcn_s_setprio(1);
+                }
+            }
+        }
         // A retired or junk stream runs with move = -inf: B = Bt = -inf keeps its rows at -inf, so
         // its J partials never reach N and never force the epilogue's group reduction.
         const float2 lm = run ? a.lentab[L] : make_float2(0.f, NINF);
@@ -582,7 +599,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             if constexpr (BIG && G == 64 && (EXP & 256)) {
                 // (timing-only: vector row index, all rows from LDS, no readfirstlane -> wrong scores)
                 RowCtx<PF> c0;
-                row(s0, c0, &tab[(min(s0.r[0], static_cast<uint32_t>(kPoisonRow)) % LDS_ROWS) * ROW_F4 + gl],
+                row(s0, c0, &tab[(min(static_cast<uint32_t>(s0.r[0]), static_cast<uint32_t>(kPoisonRow)) % LDS_ROWS) * ROW_F4 + gl],
                     Ph0{});
             } else if constexpr (BIG && G == 64) {
                 // One sequence per wave: the residue, hence the table row's home, is wave-uniform, so
@@ -818,6 +835,8 @@ static const Variant kVariants[] = {
     MSV_EXPERIMENT(16, 8, 4, 2, 1, 8192),
     MSV_EXPERIMENT(64, 24, 16, 6, 1, 8192),
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 4096),
+    MSV_EXPERIMENT(16, 88, 16, 2, 1, 16384),
+    MSV_EXPERIMENT(16, 88, 16, 2, 1, 49152),
 #endif
 };
 

@@ -1,12 +1,19 @@
 #!/bin/bash
-# Builds libmsv_hip.so from a given git revision's csrc/ into ab/<name>/ (for tools/jobs/ab.sh):
-#   bash tools/ab_build.sh <rev> <name>
+# Builds libmsv_hip.so from a given git revision's csrc/ (or the working tree: rev ".") into
+# ab/<name>/ (for tools/jobs/ab.sh); EXPERIMENTS=1 also instantiates the timing experiments:
+#   [EXPERIMENTS=1] bash tools/ab_build.sh <rev|.> <name>
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 REV=$1; NAME=$2
 TMP=$(mktemp -d)
-git -C "$ROOT" archive "$REV" hmm_fasta_viterbi_amd/csrc include | tar -x -C "$TMP"
-make -s -j8 -C "$TMP/hmm_fasta_viterbi_amd/csrc" "$TMP/hmm_fasta_viterbi_amd/lib/libmsv_hip.so" >/dev/null
+if [ "$REV" = "." ]; then
+  mkdir -p "$TMP/hmm_fasta_viterbi_amd"
+  cp -r "$ROOT/hmm_fasta_viterbi_amd/csrc" "$TMP/hmm_fasta_viterbi_amd/"
+  cp -r "$ROOT/include" "$TMP/"
+else
+  git -C "$ROOT" archive "$REV" hmm_fasta_viterbi_amd/csrc include | tar -x -C "$TMP"
+fi
+make -s -j8 EXPERIMENTS=${EXPERIMENTS:-0} -C "$TMP/hmm_fasta_viterbi_amd/csrc" "$TMP/hmm_fasta_viterbi_amd/lib/libmsv_hip.so" >/dev/null
 mkdir -p "$ROOT/ab/$NAME"
 cp "$TMP/hmm_fasta_viterbi_amd/lib/libmsv_hip.so" "$ROOT/ab/$NAME/"
 rm -rf "$TMP"

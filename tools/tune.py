@@ -72,17 +72,18 @@ def main():
                 got = s.cpu().numpy()
                 if ref_scores is None:
                     ref_scores = got.copy()
-                same = bool(np.array_equal(got.view(np.uint32), ref_scores.view(np.uint32))) or name.startswith("exp")
-                res[name].append((use_order, ms, same))
+                raw = bool(np.array_equal(got.view(np.uint32), ref_scores.view(np.uint32)))
+                res[name].append((use_order, ms, raw or name.startswith("exp"), raw))
     out = []
     for name in names:
         for use_order in (False, True):
-            t = [ms for (u, ms, same) in res[name] if u == use_order]
-            same = all(sm for (u, ms, sm) in res[name])
+            t = [ms for (u, ms, _, _) in res[name] if u == use_order]
+            same = all(sm for (_, _, sm, _) in res[name])
+            raw = all(rw for (_, _, _, rw) in res[name])
             best = min(t)
             out.append({"variant": name, "order": use_order, "ms_min": round(best, 4),
                         "ms_med": round(float(np.median(t)), 4), "Tcell_s": round(cells / best / 1e9, 3),
-                        "valu_frac": round(3 * cells / best / 1e9 / 78.64, 4), "bitwise_same": same})
+                        "valu_frac": round(3 * cells / best / 1e9 / 78.64, 4), "bitwise_same": same, "bitwise_same_raw": raw})
     out.sort(key=lambda d: d["ms_min"])
     for d in out:
         print(json.dumps(d))
