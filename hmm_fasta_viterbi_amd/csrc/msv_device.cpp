@@ -172,15 +172,16 @@ struct msv_profile {
 // (never win a max); row 20 is the +inf poison row for codes >= 20.
 // Split variants (v->sa > 0, G = 32/64, lane gl owns states gl*S + 1 .. gl*S + S as usual): an A table
 // [20 rows][SA/4][G] float4 (the lane's first SA states, staged in LDS) followed by a B table
-// [21 rows][(S-SA)/2][G] float2 (its last S - SA states, read from L2; row 20 = poison).
+// [21 rows][G][HBP] float2 (its last S - SA states as HB = (S-SA)/2 halves padded to HBP = even,
+// lane-contiguous so a lane reads them as HBP/2 float4 loads from L2; row 20 = poison).
 static msv_status install_plan(msv_profile* p, const msvk::Variant* v, Plan& plan) {
     const uint32_t model_length = p->model_length, R = model_length - 1;
     const int G = v->G, S = v->S, C4 = S / 4;
     const float ninf = -std::numeric_limits<float>::infinity();
     const float pinf = std::numeric_limits<float>::infinity();
     std::vector<float> tab;
-    // one [rows][chunks][G] block of `width`-float chunks (float4, or float2 for a split B table) whose
-    // lane gl, chunk c, slot q holds state first + gl*span + width*c + q
+    // one [rows][chunks][G] block of `width`-float chunks whose lane gl, chunk c, slot q holds state
+    // first + gl*span + width*c + q
     auto block = [&](int rows, int chunks, uint32_t first, int span, int width) {
         for (int r = 0; r < rows; ++r)
             for (int c = 0; c < chunks; ++c)
@@ -195,7 +196,20 @@ static msv_status install_plan(msv_profile* p, const msvk::Variant* v, Plan& pla
     };
     if (v->sa > 0) {
         block(msvk::kAminoAcids, v->sa / 4, 1, S, 4);
-        block(msvk::kTableRows, (S - v->sa) / 2, static_cast<uint32_t>(v->sa + 1), S, 2);
+        // B table [21 rows][G][HBP] float2, lane-contiguous (each lane reads HBP/2 float4), HBP = the
+        // lane's HB = (S - SA)/2 halves rounded up to even (the pad half is -inf and never read)
+        const int HB = (S - v->sa) / 2, HBP = (HB + 1) & ~1;
+        for (int r = 0; r < msvk::kTableRows; ++r)
+            for (int gl = 0; gl < G; ++gl)
+                for (int h = 0; h < HBP; ++h)
+                    for (int q = 0; q < 2; ++q) {
+                        const uint32_t j = static_cast<uint32_t>(v->sa + 1 + gl * S + 2 * h + q);  // state 1..
+                        float val;
+                        if (r == msvk::kPoisonRow) val = pinf;
+                        else if (h < HB && j <= R) val = p->emission_scores[static_cast<size_t>(r) * model_length + j];
+                        else val = ninf;
+                        tab.push_back(val);
+                    }
     } else {
         block(msvk::kTableRows, C4, 1, S, 4);
     }

@@ -190,7 +190,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     constexpr int CA = SPLIT ? SA / 4 : C4;  // float4 chunks per lane whose emissions are staged in LDS
     constexpr int HB = SPLIT ? (S - SA) / 2 : 0;  // SPLIT: float2 halves per lane read from the B table
     constexpr int ROW_F4 = CA * G;           // float4 per LDS residue row
-    constexpr int ROW_B = HB * G;            // float2 per global B-table residue row
+    constexpr int HBP = (HB + 1) & ~1;       // SPLIT: halves per lane in the B table (padded to even)
     constexpr int LDS_ROWS = SPLIT ? kAminoAcids : lds_rows_for(G, S);
     // Cross-row emission prefetch: when the ring holds a whole row (small profiles), the NEXT row's
     // chunks are requested right after this row's last cell update, so the LDS latency hides behind
@@ -310,18 +310,30 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     auto lds_row = [&](uint32_t r) -> const float4* {
         return &tab[min(r, static_cast<uint32_t>(SPLIT ? kAminoAcids - 1 : kPoisonRow)) * ROW_F4 + gl];
     };
-    // SPLIT: the B table ([21][HB][G] float2: 2-state halves, so the padding past LENG stays under
-    // 2 states per lane) follows the 20 LDS rows in a.etab; the current row's B halves live in
-    // `bring`, requested one row ahead.
+    // SPLIT: the B table ([21][G][HBP] float2: 2-state halves, so the padding past LENG stays under
+    // 2 states per lane; lane-contiguous, read as float4) follows the 20 LDS rows in a.etab; the
+    // current row's B halves live in `bring`, requested one row ahead.
     const float2* __restrict__ etabB = reinterpret_cast<const float2*>(a.etab + kAminoAcids * ROW_F4);
     struct BRing {
         float2 v[HB > 0 ? HB : 1];
     } bring;
     auto fill_b = [&](uint32_t r) {
-        if constexpr (SPLIT) {
-            const float2* bp = &etabB[min(r, static_cast<uint32_t>(kPoisonRow)) * ROW_B + gl];
+        if constexpr (SPLIT && (EXP & 65536)) {
+            // timing-only: B halves read from the LDS A rows (wrong scores) -- the cost of the L2 reads
+            const float2* bp = reinterpret_cast<const float2*>(&tab[min(r, static_cast<uint32_t>(kAminoAcids - 1)) * ROW_F4]) + gl;
 #pragma unroll
             for (int q = 0; q < HB; ++q) bring.v[q] = bp[q * G];
+        } else if constexpr (SPLIT) {
+            // lane-contiguous halves: HBP/2 float4 loads per lane (half the VMEM issues of float2 loads
+            // strided by G: cfg5 25.08 vs 25.56 ms, profiles/r01_exp_split_b.jsonl)
+            const float4* bp = reinterpret_cast<const float4*>(etabB) +
+                               (min(r, static_cast<uint32_t>(kPoisonRow)) * G + gl) * (HBP / 2);
+#pragma unroll
+            for (int q = 0; q < HBP / 2; ++q) {
+                const float4 v = bp[q];
+                bring.v[2 * q] = make_float2(v.x, v.y);
+                if (2 * q + 1 < HB) bring.v[2 * q + 1] = make_float2(v.z, v.w);
+            }
         }
     };
     auto row_ptr = [&](St& st, auto ph) -> const float4* {
@@ -814,6 +826,10 @@ hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t
     Variant{G_, S_, W_, P_, 1, kAminoAcids, false,                                                        \
             reinterpret_cast<const void*>(&msv_batch_kernel<G_, S_, W_, P_, false, 1, SA_>),               \
             "msv_g" #G_ "_s" #S_ "_a" #SA_ "_w" #W_ "_p" #P_ "_d1", SA_}
+#define MSV_SPLIT_EXPERIMENT(G_, S_, SA_, W_, P_, X_)                                                     \
+    Variant{G_, S_, W_, P_, 1, kAminoAcids, false,                                                        \
+            reinterpret_cast<const void*>(&msv_batch_kernel<G_, S_, W_, P_, false, 1, SA_, X_>),           \
+            "exp" #X_ "_g" #G_ "_s" #S_ "_a" #SA_ "_w" #W_ "_p" #P_ "_d1", SA_}
 
 static const Variant kVariants[] = {
 #include "msv_variants.inc"
@@ -837,6 +853,7 @@ static const Variant kVariants[] = {
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 4096),
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 16384),
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 49152),
+    MSV_SPLIT_EXPERIMENT(32, 76, 64, 16, 2, 65536),
 #endif
 };
 
