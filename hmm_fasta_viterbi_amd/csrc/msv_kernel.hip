@@ -307,8 +307,16 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // 32-bit value, each measured 2-4% slower on 1400.hmm: they move the residue-load wait.)
     // (SPLIT: the LDS holds rows 0..19 only; codes >= 20 read row 19 there and the +inf poison row
     // of the B table, which still makes the score +inf.)
+    // (EXP & 262144: timing A/B, the row * ROW_F4 + gl index form -> v_mul_u32_u24 + v_or per row
+    // instead of one v_mad_u32_u24 on a hoisted lane byte offset)
+    const uint32_t lds_lane = static_cast<uint32_t>(gl * 16);
     auto lds_row = [&](uint32_t r) -> const float4* {
-        return &tab[min(r, static_cast<uint32_t>(SPLIT ? kAminoAcids - 1 : kPoisonRow)) * ROW_F4 + gl];
+        const uint32_t rr = min(r, static_cast<uint32_t>(SPLIT ? kAminoAcids - 1 : kPoisonRow));
+        if constexpr ((EXP & 262144) != 0) return &tab[rr * ROW_F4 + gl];
+        // (left to itself the compiler emits v_mul_u32_u24 + v_or for this sum of disjoint bits)
+        uint32_t off;
+        asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(off) : "v"(rr), "s"(static_cast<uint32_t>(ROW_F4 * 16)), "v"(lds_lane));
+        return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(tab) + off);
     };
     // SPLIT: the B table ([21][G][HBP] float2: 2-state halves, so the padding past LENG stays under
     // 2 states per lane; lane-contiguous, read as float4) follows the 20 LDS rows in a.etab; the
@@ -317,6 +325,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     struct BRing {
         float2 v[HB > 0 ? HB : 1];
     } bring;
+    const uint32_t b_lane = static_cast<uint32_t>(gl * HBP * 8);  // SPLIT: the lane's B halves, in bytes
     auto fill_b = [&](uint32_t r) {
         if constexpr (SPLIT && (EXP & 65536)) {
             // timing-only: B halves read from the LDS A rows (wrong scores) -- the cost of the L2 reads
@@ -326,8 +335,9 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         } else if constexpr (SPLIT) {
             // lane-contiguous halves: HBP/2 float4 loads per lane (half the VMEM issues of float2 loads
             // strided by G: cfg5 25.08 vs 25.56 ms, profiles/r01_exp_split_b.jsonl)
-            const float4* bp = reinterpret_cast<const float4*>(etabB) +
-                               (min(r, static_cast<uint32_t>(kPoisonRow)) * G + gl) * (HBP / 2);
+            // byte offset = row * (G * HBP * 8) + the lane's hoisted offset: one v_mad_u32_u24
+            const uint32_t off = min(r, static_cast<uint32_t>(kPoisonRow)) * static_cast<uint32_t>(G * HBP * 8) + b_lane;
+            const float4* bp = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(etabB) + off);
 #pragma unroll
             for (int q = 0; q < HBP / 2; ++q) {
                 const float4 v = bp[q];
