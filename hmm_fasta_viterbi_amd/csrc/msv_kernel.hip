@@ -371,8 +371,10 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         }
         rc.ep = ep;
         rc.Bt = st.B + trBMk;
-        if constexpr (G >= 16) {
-            st.nbr = shift_in<G>(st.M[S - 1], st.nbr);
+        if constexpr (G >= 16 || (EXP & 524288)) {
+            // (EXP & 524288, G = 8: timing A/B, a plain row_shr:1 -- exact only when every group's last
+            // state is padding (-inf emissions), so the last lane of a group always sends -inf)
+            st.nbr = (G >= 16) ? shift_in<G>(st.M[S - 1], st.nbr) : dpp<DPP_ROW_SHR1>(st.nbr, st.M[S - 1]);
             rc.nbr = st.nbr;
         } else {
             rc.nbr = shift_in<G>(st.M[S - 1], NINF);
@@ -864,6 +866,9 @@ static const Variant kVariants[] = {
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 16384),
     MSV_EXPERIMENT(16, 88, 16, 2, 1, 49152),
     MSV_SPLIT_EXPERIMENT(32, 76, 64, 16, 2, 65536),
+    MSV_EXPERIMENT(8, 176, 8, 2, 1, 524288),
+    MSV_EXPERIMENT(8, 176, 8, 3, 1, 524288),
+    MSV_EXPERIMENT(8, 176, 8, 4, 1, 524288),
 #endif
 };
 
