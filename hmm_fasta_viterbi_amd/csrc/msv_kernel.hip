@@ -26,14 +26,16 @@
 //   * The 20 x (G*S) fp32 emission table (+1 poison row of +inf for codes >= 20) lives in LDS,
 //     laid out [residue][chunk][lane] float4 so every ds_read_b128 of a group is contiguous.
 //     One workgroup per CU shares the table across all its waves.  Profiles whose table does not
-//     fit the 160 KiB LDS ("BIG", LENG > ~1950) keep the rows that fit in LDS and read the rest
-//     through generic (flat) loads from L2.
+//     fit the 160 KiB LDS (LENG > ~1920) use the SPLIT layout: each lane's first SA states have all
+//     20 rows in LDS, its last S - SA states come from a lane-contiguous global table (L2), read one
+//     row ahead as float4; beyond 3072 states the G = 64 row-class layout serves whole rows from LDS
+//     or L2 behind a wave-uniform branch.
 //   * Persistent grid: every group dequeues sequences from a device counter (prefetched one
 //     sequence ahead, one atomic per sequence), so long and short sequences load-balance with no
 //     host scheduling; a group that reaches the end of its sequence writes the score and starts
 //     the next one in place.
 //   * The residue stream is read one byte per row per group (global_load_ubyte, L1/L2-served,
-//     two rows of prefetch); the per-length transition constants come from a host-computed table
+//     1-6 rows of prefetch into rotating slots, by row length); the per-length transition constants come from a host-computed table
 //     (host logf, so scores never depend on a device logf).
 #include <hip/hip_runtime.h>
 
