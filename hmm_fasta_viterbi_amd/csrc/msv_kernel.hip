@@ -16,7 +16,7 @@
 // max(N+move, J+move) == fl(max(N,J) + move) bit for bit; no multiply exists, so no contraction.
 //
 // Mapping (MI355X-first, not a translation of the OpenCL NDRange-per-residue):
-//   * A "group" of G lanes (G = 16 or 32) owns ONE sequence; lane gl holds the S consecutive
+//   * A "group" of G lanes (G = 16, 32 or 64; 4/8 for small profiles) owns ONE sequence; lane gl holds the S consecutive
 //     match states gl*S+1 .. gl*S+S of the DP row in VGPRs (float M[S]).  A 64-lane wave runs
 //     64/G independent sequences.
 //   * The j-1 neighbour crosses a lane boundary once per row: one DPP row_shr:1 (+ row_bcast:15
@@ -35,8 +35,9 @@
 //     host scheduling; a group that reaches the end of its sequence writes the score and starts
 //     the next one in place.
 //   * The residue stream is read one byte per row per group (global_load_ubyte, L1/L2-served,
-//     1-6 rows of prefetch into rotating slots, by row length); the per-length transition constants come from a host-computed table
-//     (host logf, so scores never depend on a device logf).
+//     1-6 rows of prefetch into rotating slots, by row length); the per-length transition
+//     constants come from a host-computed table (host logf, so scores never depend on a device
+//     logf).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
