@@ -104,7 +104,6 @@ const msvk::Variant* pick_latency_variant(uint32_t states) {
     for (int i = 0; i < count; ++i) {
         const msvk::Variant& v = all[i];
         if (v.G != 64 || static_cast<uint32_t>(v.G * v.S) < states) continue;
-        if (std::strncmp(v.name, "exp", 3) == 0) continue;
         if (!best || variant_cost(v) < variant_cost(*best)) best = &v;
     }
     return best;
@@ -117,7 +116,6 @@ const msvk::Variant* pick_variant(uint32_t states) {
     for (int i = 0; i < count; ++i) {
         const msvk::Variant& v = all[i];
         if (static_cast<uint32_t>(v.G * v.S) < states) continue;
-        if (std::strncmp(v.name, "exp", 3) == 0) continue;  // timing-only experiments
         // 4/8-lane groups are tuning candidates only: their per-lane rows are longer, which the issue
         // model rewards, but small profiles are latency-bound and they measured no faster (100.hmm:
         // g8_s16 0.162 ms, g16_s8 0.165 ms, g4_s28 0.219 ms).

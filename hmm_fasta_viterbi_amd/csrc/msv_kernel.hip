@@ -170,7 +170,7 @@ template <int PF>
 struct RowCtx {
     static constexpr int kPF = PF;
     const float4* ep;
-    float Bt, nbr, p0, p1, p2, p3;
+    float Bt, nbr, p0, p1;
     uint8_t rnext;   // residue code RPF rows ahead
     float4 ring[PF];
 };
@@ -180,12 +180,11 @@ struct RowCtx {
 // LDS, its last S - SA states (the "B block") are read from the global table (L2) for every row -- no
 // per-row LDS/L2 class branch, so the groups of a wave run the same row body whatever their residues;
 // the next row's B halves are requested one row ahead.
-template <int G, int S, int WAVES, int PF, bool BIG, int D, int SA = 0, int EXP = 0>
+template <int G, int S, int WAVES, int PF, bool BIG, int D, int SA = 0>
 __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs a) {
     constexpr bool SPLIT = SA > 0;
-    // (EXP & 64: timing-only A/B, one row of residue prefetch; 2 rows measured no faster at S=88)
     // SPLIT needs the next row's residue one row early (B-chunk prefetch): at least 2 rows.
-    using St = Stream<S, (EXP & 64) ? 1 : ((SPLIT && residue_prefetch<S>() < 2) ? 2 : residue_prefetch<S>())>;
+    using St = Stream<S, (SPLIT && residue_prefetch<S>() < 2) ? 2 : residue_prefetch<S>()>;
     static_assert(SPLIT ? (S - SA) % 2 == 0 : S % 4 == 0, "float4 chunks (A block), float2 halves (B block)");
     static_assert(PF >= 1 && D >= 1 && D <= 2, "PF >= 1, D in {1, 2}");
     static_assert(!SPLIT || (G >= 32 && !BIG && D == 1 && SA % 4 == 0 && SA < S), "split: 32/64-lane groups");
@@ -260,23 +259,6 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             atomicOr(a.errors, kErrTooLong);
         }
         const bool run = !retire && !empty && !too_long;
-        if constexpr ((EXP & 16384) != 0) {
-            // Tail priority: the groups that dequeue the last indices hold the most remaining rows
-            // when the queue drains, so their waves get VALU issue priority over older waves
-            // (arbitration is priority, then age): 1 / 2 / 3 for the last K, K/2, K/4 indices,
-            // K = groups in flight.  Priority only rises, since indices rise.
-            const uint32_t K = gridDim.x * WAVES * (64 / G) * ((EXP & 32768) ? 2u : 1u);
-            const uint32_t n = a.n;
-            if (n > K) {
-                if (__any(run && idx >= n - K / 4)) {
-                    __builtin_amdgcn_s_setprio(3);
-                } else if (__any(run && idx >= n - K / 2)) {
-                    __builtin_amdgcn_s_setprio(2);
-                } else if (__any(run && idx >= n - K)) {
-                    __builtin_amdgcn_s_setprio(1);
-                }
-            }
-        }
         // A retired or junk stream runs with move = -inf: B = Bt = -inf keeps its rows at -inf, so
         // its J partials never reach N and never force the epilogue's group reduction.
         const float2 lm = run ? a.lentab[L] : make_float2(0.f, NINF);
@@ -310,13 +292,11 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // 32-bit value, each measured 2-4% slower on 1400.hmm: they move the residue-load wait.)
     // (SPLIT: the LDS holds rows 0..19 only; codes >= 20 read row 19 there and the +inf poison row
     // of the B table, which still makes the score +inf.)
-    // (EXP & 262144: timing A/B, the row * ROW_F4 + gl index form -> v_mul_u32_u24 + v_or per row
-    // instead of one v_mad_u32_u24 on a hoisted lane byte offset)
+    // The address is one v_mad_u32_u24 on a hoisted lane byte offset (the index form
+    // rr * ROW_F4 + gl compiled to v_mul_u32_u24 + v_or: profiles/r01_ab_row_address.jsonl).
     const uint32_t lds_lane = static_cast<uint32_t>(gl * 16);
     auto lds_row = [&](uint32_t r) -> const float4* {
         const uint32_t rr = min(r, static_cast<uint32_t>(SPLIT ? kAminoAcids - 1 : kPoisonRow));
-        if constexpr ((EXP & 262144) != 0) return &tab[rr * ROW_F4 + gl];
-        // (left to itself the compiler emits v_mul_u32_u24 + v_or for this sum of disjoint bits)
         uint32_t off;
         asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(off) : "v"(rr), "s"(static_cast<uint32_t>(ROW_F4 * 16)), "v"(lds_lane));
         return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(tab) + off);
@@ -330,12 +310,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     } bring;
     const uint32_t b_lane = static_cast<uint32_t>(gl * HBP * 8);  // SPLIT: the lane's B halves, in bytes
     auto fill_b = [&](uint32_t r) {
-        if constexpr (SPLIT && (EXP & 65536)) {
-            // timing-only: B halves read from the LDS A rows (wrong scores) -- the cost of the L2 reads
-            const float2* bp = reinterpret_cast<const float2*>(&tab[min(r, static_cast<uint32_t>(kAminoAcids - 1)) * ROW_F4]) + gl;
-#pragma unroll
-            for (int q = 0; q < HB; ++q) bring.v[q] = bp[q * G];
-        } else if constexpr (SPLIT) {
+        if constexpr (SPLIT) {
             // lane-contiguous halves: HBP/2 float4 loads per lane (half the VMEM issues of float2 loads
             // strided by G: cfg5 25.08 vs 25.56 ms, profiles/r01_exp_split_b.jsonl)
             // byte offset = row * (G * HBP * 8) + the lane's hoisted offset: one v_mad_u32_u24
@@ -364,32 +339,17 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         for (int q = 0; q < (P < CA ? P : CA); ++q) rc.ring[q] = ep[(CA - 1 - q) * G];
     };
     auto prologue = [&](St& st, auto& rc, const float4* ep, auto ph) {
-        // (EXP & 32: timing-only, synthetic residues instead of the stream -> wrong scores)
-        if constexpr (EXP & 32) {
-            rc.rnext = (st.pos * 7u) % 20u;
-        } else if constexpr (EXP & 8192) {  // timing-only: no residue load, no arithmetic either
-            rc.rnext = st.r[(decltype(ph)::value + St::RPF - 1) % St::RPF] ^ 1u;
-        } else {
-            rc.rnext = res[min(st.pos + St::RPF, st.endpos)];
-        }
+        (void)ph;
+        rc.rnext = res[min(st.pos + St::RPF, st.endpos)];
         rc.ep = ep;
         rc.Bt = st.B + trBMk;
-        if constexpr (G >= 16 || (EXP & 524288)) {
-            // (EXP & 524288, G = 8: timing A/B, a plain row_shr:1 -- exact only when every group's last
-            // state is padding (-inf emissions), so the last lane of a group always sends -inf)
-            st.nbr = (G >= 16) ? shift_in<G>(st.M[S - 1], st.nbr) : dpp<DPP_ROW_SHR1>(st.nbr, st.M[S - 1]);
+        if constexpr (G >= 16) {
+            st.nbr = shift_in<G>(st.M[S - 1], st.nbr);
             rc.nbr = st.nbr;
         } else {
             rc.nbr = shift_in<G>(st.M[S - 1], NINF);
         }
-        // p0/p1 start from the row's first chunk (a plain max, no -inf seed); the EXP & 4 timing
-        // experiment seeds all four
-        if constexpr (EXP & 4) {
-            rc.p0 = NINF;
-            rc.p1 = NINF;
-            rc.p2 = NINF;
-            rc.p3 = NINF;
-        }
+        // p0/p1 start from the row's first chunk (a plain max, no -inf seed)
         if constexpr (!XROW) fill_ring(rc, ep);
     };
     // One float4 chunk (states 4c+1 .. 4c+4 of the lane), highest state first so M[k-1] is still
@@ -399,10 +359,9 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         constexpr int c = decltype(cc)::value;
         constexpr int slot = (CA - 1 - c) % P;
         const float4 ev = rc.ring[slot];
-        // (EXP & 1: timing-only experiment, emissions not re-read -> wrong scores, never shipped)
-        if constexpr (c - P >= 0 && !(EXP & 1)) rc.ring[slot] = rc.ep[(c - P) * G];
+        if constexpr (c - P >= 0) rc.ring[slot] = rc.ep[(c - P) * G];
         constexpr int k = 4 * c;
-        if constexpr (!(EXP & (4 | 2048)) && !BIG && S >= 64) {
+        if constexpr (!BIG && S >= 64) {
             // The chunk's 10 VALU ops in a fixed interleaved order (max, max, add, max, add, max, add,
             // max3, add, max3).  gfx950 issues v_max/v_max3 at half the v_add rate and overlaps the two
             // kinds when they alternate; in isolation the compiler's grouping ([4 max][4 add][2 max3])
@@ -448,7 +407,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             }
             return;
         }
-        // (EXP & 2048: timing-only A/B, the compiler-scheduled C++ form of the same chunk)
+        // small rows and BIG rows: the compiler-scheduled form of the same chunk
         st.M[k + 3] = ev.w + fmaxf(st.M[k + 2], rc.Bt);
         st.M[k + 2] = ev.z + fmaxf(st.M[k + 1], rc.Bt);
         st.M[k + 1] = ev.y + fmaxf(st.M[k], rc.Bt);
@@ -457,10 +416,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         } else {
             st.M[k] = ev.x + fmaxf(st.M[k - 1], rc.Bt);
         }
-        if constexpr ((EXP & 4) && (c & 1)) {  // 4 accumulators: half-length E dependency chains
-            rc.p2 = fmaxf(fmaxf(rc.p2, st.M[k + 3]), st.M[k + 2]);
-            rc.p3 = fmaxf(fmaxf(rc.p3, st.M[k + 1]), st.M[k]);
-        } else if constexpr (!SPLIT && c == CA - 1 && !(EXP & 4)) {  // the row's first chunk: no -inf seed
+        if constexpr (!SPLIT && c == CA - 1) {  // the row's first chunk: no -inf seed
             rc.p0 = fmaxf(st.M[k + 3], st.M[k + 2]);
             rc.p1 = fmaxf(st.M[k + 1], st.M[k]);
         } else {
@@ -490,7 +446,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     };
     // Row epilogue: E over the group, the specials (MSV_HMM.cpp:107-110), cursor advance.
     auto epilogue = [&](St& st, auto& rc, auto ph) {
-        const float Elane = (EXP & 4) ? fmaxf(fmaxf(rc.p0, rc.p1), fmaxf(rc.p2, rc.p3)) : fmaxf(rc.p0, rc.p1);
+        const float Elane = fmaxf(rc.p0, rc.p1);
         // Per-lane partials (see Stream): J_l, and C_l unless C == J (tr_E_C == tr_E_J, which is
         // always the case for the reference's nu = 2, MSV_HMM.cpp:49-53: then the C and J
         // recurrences are identical and C is read from J at the end).
@@ -506,14 +462,11 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         // reduction across lanes (DPP butterfly) leaves the row's dependency chain.
         // (G = 64: a row_bcast:15/31 + v_readlane reduction to an SGPR measured 13% slower on
         // 2405.hmm than the permlane swaps -- the SGPR round trip stalls the row)
-        // (EXP & 4096: timing-only, B = N + move on every row with no test -- right only while no
-        // J_l reaches N, i.e. on random-like sequences: the cost of the per-row test and branch)
         // The common value first and the rare one as an overwrite, so the common path falls through
-        // (as an if/else the else-block was laid out of line: two taken branches per row).
+        // (as an if/else the else-block was laid out of line: two taken branches per row).  The test
+        // and branch cost 6% of the cfg2 kernel, 0.5% of cfg3 (profiles/r01_exp_speculative_b.jsonl).
         st.B = st.N + st.move;
-        if constexpr (!(EXP & 4096)) {
-            if (__builtin_expect(__any(st.J >= st.N), 0)) st.B = fmaxf(st.N, group_max<G>(st.J)) + st.move;
-        }
+        if (__builtin_expect(__any(st.J >= st.N), 0)) st.B = fmaxf(st.N, group_max<G>(st.J)) + st.move;
         ++st.pos;
         if constexpr (ROT) {
             st.r[decltype(ph)::value] = rc.rnext;  // this row's slot now holds the row RPF ahead
@@ -572,9 +525,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             __builtin_amdgcn_sched_barrier(0);
         }
         [&]<int... I>(std::integer_sequence<int, I...>) {
-            ((chunk(st, rc, std::integral_constant<int, CA - 1 - I>{}),
-              [&] { if constexpr (!(EXP & 2) || (I & 1)) __builtin_amdgcn_sched_barrier(0); }()),
-             ...);
+            ((chunk(st, rc, std::integral_constant<int, CA - 1 - I>{}), __builtin_amdgcn_sched_barrier(0)), ...);
         }(std::make_integer_sequence<int, CA>{});
         epilogue(st, rc, ph);
     };
@@ -623,28 +574,21 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
                 (void)(step(std::integral_constant<int, I>{}) && ...);
             }(std::make_integer_sequence<int, St::RPF>{});
         } else {
-            if constexpr (BIG && G == 64 && (EXP & 256)) {
-                // (timing-only: vector row index, all rows from LDS, no readfirstlane -> wrong scores)
-                RowCtx<PF> c0;
-                row(s0, c0, &tab[(min(static_cast<uint32_t>(s0.r[0]), static_cast<uint32_t>(kPoisonRow)) % LDS_ROWS) * ROW_F4 + gl],
-                    Ph0{});
-            } else if constexpr (BIG && G == 64) {
+            if constexpr (BIG && G == 64) {
                 // One sequence per wave: the residue, hence the table row's home, is wave-uniform, so
                 // the LDS rows and the L2 rows run as two separate (scalar-branched) row bodies with
                 // precise waits -- no generic loads, no per-lane selects.  An L2 row requests up to 10
                 // chunks up front to pay the L2 latency about once per row.
                 // (a vector compare with exec masking instead of readfirstlane measured 1.5% slower;
-                // reading the class one row early into an SGPR changed nothing; without the class
-                // branch at all -- EXP & 256, wrong scores -- the row is 10% faster)
+                // reading the class one row early into an SGPR changed nothing; a timing-only form
+                // with no class branch at all, wrong scores, ran the row 10% faster)
                 const uint32_t rr =
                     __builtin_amdgcn_readfirstlane(min(s0.r[0], static_cast<uint32_t>(kPoisonRow)));
-                // (EXP & 8: timing-only, every row served from LDS -> wrong scores; EXP & 16: L2 rows
-                // with the LDS ring depth)
-                if ((EXP & 8) || rr < static_cast<uint32_t>(LDS_ROWS)) {
+                if (rr < static_cast<uint32_t>(LDS_ROWS)) {
                     RowCtx<PF> c0;
-                    row(s0, c0, &tab[((EXP & 8) ? rr % LDS_ROWS : rr) * ROW_F4 + gl], Ph0{});
+                    row(s0, c0, &tab[rr * ROW_F4 + gl], Ph0{});
                 } else {
-                    RowCtx<(EXP & 16) ? PF : (C4 < 10 ? C4 : 10)> c0;
+                    RowCtx<(C4 < 10 ? C4 : 10)> c0;
                     row(s0, c0, &a.etab[rr * ROW_F4 + gl], Ph0{});
                 }
             } else if constexpr (D == 1) {
@@ -656,8 +600,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
                 prologue(s1, c1, row_ptr(s1, Ph0{}), Ph0{});
                 [&]<int... I>(std::integer_sequence<int, I...>) {
                     ((chunk(s0, c0, std::integral_constant<int, C4 - 1 - I>{}),
-                      chunk(s1, c1, std::integral_constant<int, C4 - 1 - I>{}),
-                      [&] { if constexpr (!(EXP & 2) || (I & 1)) __builtin_amdgcn_sched_barrier(0); }()),
+                      chunk(s1, c1, std::integral_constant<int, C4 - 1 - I>{}), __builtin_amdgcn_sched_barrier(0)),
                      ...);
                 }(std::make_integer_sequence<int, C4>{});
                 epilogue(s0, c0, Ph0{});
@@ -830,49 +773,14 @@ hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t
                 &msv_batch_kernel<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_>),               \
             "msv_g" #G_ "_s" #S_ "_w" #W_ "_p" #P_ "_d" #D_}
 
-#define MSV_EXPERIMENT(G_, S_, W_, P_, D_, X_)                                                            \
-    Variant{G_, S_, W_, P_, D_, lds_rows_for(G_, S_), lds_rows_for(G_, S_) < kTableRows,                  \
-            reinterpret_cast<const void*>(                                                                 \
-                &msv_batch_kernel<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_, 0, X_>),        \
-            "exp" #X_ "_g" #G_ "_s" #S_ "_w" #W_ "_p" #P_ "_d" #D_}
-
 // Split layout (G = 32 or 64): SA states per lane from LDS (20 rows), S - SA from L2.
 #define MSV_SPLIT_VARIANT(G_, S_, SA_, W_, P_)                                                            \
     Variant{G_, S_, W_, P_, 1, kAminoAcids, false,                                                        \
             reinterpret_cast<const void*>(&msv_batch_kernel<G_, S_, W_, P_, false, 1, SA_>),               \
             "msv_g" #G_ "_s" #S_ "_a" #SA_ "_w" #W_ "_p" #P_ "_d1", SA_}
-#define MSV_SPLIT_EXPERIMENT(G_, S_, SA_, W_, P_, X_)                                                     \
-    Variant{G_, S_, W_, P_, 1, kAminoAcids, false,                                                        \
-            reinterpret_cast<const void*>(&msv_batch_kernel<G_, S_, W_, P_, false, 1, SA_, X_>),           \
-            "exp" #X_ "_g" #G_ "_s" #S_ "_a" #SA_ "_w" #W_ "_p" #P_ "_d1", SA_}
 
 static const Variant kVariants[] = {
 #include "msv_variants.inc"
-#ifdef MSV_WITH_EXPERIMENTS
-    // timing-only experiments (wrong scores by construction; selected only by name in tools/;
-    // build with `make EXPERIMENTS=1`)
-    MSV_EXPERIMENT(16, 88, 16, 2, 1, 1),
-    MSV_EXPERIMENT(16, 88, 16, 4, 1, 2),
-    MSV_EXPERIMENT(16, 88, 16, 2, 1, 4),
-    MSV_EXPERIMENT(16, 88, 16, 4, 1, 6),
-    MSV_EXPERIMENT(16, 88, 16, 3, 1, 4),
-    MSV_EXPERIMENT(64, 40, 16, 2, 1, 8),
-    MSV_EXPERIMENT(64, 40, 16, 2, 1, 256),
-    MSV_EXPERIMENT(16, 8, 4, 2, 1, 32),
-    MSV_EXPERIMENT(16, 8, 16, 2, 1, 32),
-    MSV_EXPERIMENT(16, 88, 16, 2, 1, 32),
-    MSV_EXPERIMENT(16, 88, 16, 2, 1, 2048),
-    MSV_EXPERIMENT(16, 8, 4, 2, 1, 4096),
-    MSV_EXPERIMENT(16, 8, 4, 2, 1, 8192),
-    MSV_EXPERIMENT(64, 24, 16, 6, 1, 8192),
-    MSV_EXPERIMENT(16, 88, 16, 2, 1, 4096),
-    MSV_EXPERIMENT(16, 88, 16, 2, 1, 16384),
-    MSV_EXPERIMENT(16, 88, 16, 2, 1, 49152),
-    MSV_SPLIT_EXPERIMENT(32, 76, 64, 16, 2, 65536),
-    MSV_EXPERIMENT(8, 176, 8, 2, 1, 524288),
-    MSV_EXPERIMENT(8, 176, 8, 3, 1, 524288),
-    MSV_EXPERIMENT(8, 176, 8, 4, 1, 524288),
-#endif
 };
 
 const Variant* variants(int* count) {

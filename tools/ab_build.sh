@@ -1,6 +1,7 @@
 #!/bin/bash
 # Builds libmsv_hip.so from a given git revision's csrc/ (or the working tree: rev ".") into
-# ab/<name>/ (for tools/jobs/ab.sh); EXPERIMENTS=1 also instantiates the timing experiments:
+# ab/<name>/ (for tools/jobs/ab.sh); EXPERIMENTS=1 also instantiates the round-1 timing experiments
+# (revisions up to a91649a only):
 #   [EXPERIMENTS=1] bash tools/ab_build.sh <rev|.> <name>
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
