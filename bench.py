@@ -6,9 +6,12 @@
 A step = one pass of the hot path over one batch resident in HBM: the longest-first dequeue
 order (device counting sort) + ONE fused MSV kernel launch scoring every sequence of the rank's
 shard against the profile.  Sequences are independent, so the batch shards across ranks with no
-data-path collective (weak scaling: every rank scores its own 100k sequences); the scores are
-gathered to rank 0 over RCCL once after timing, outside the timed region, and reported
-separately.
+data-path collective.
+  cfg2/cfg3/cfg5 (weak scaling): every rank scores its own seeded batch of the config's size; the
+      scores are gathered to rank 0 over RCCL once after timing (reported as gather_ms).
+  cfg4 (strong scaling, BASELINE configs[3]): ONE seeded 1M-sequence set, cut into residue-balanced
+      contiguous shards (distributed.shard_bounds == msv_shard_bounds); the RCCL gather of the
+      scores to every rank is part of every timed step.
 
 Rank 0 prints ONE JSON line with the contract keys plus:
   roofline     -- the dominant kernel against the fp32 VALU issue roofline:
@@ -34,11 +37,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {
-    # name: (profile, sequences per GPU, lmin, lmax, seed)  -- SURVEY 8(d) / BASELINE.md
-    "cfg2": ("100.hmm", 10_000, 300, 500, 1),
-    "cfg3": ("1400.hmm", 100_000, 300, 500, 2),
-    "cfg4": ("1400.hmm", 125_000, 300, 500, 3),   # 1M over 8 GPUs
-    "cfg5": ("2405.hmm", 100_000, 1500, 2500, 4),
+    # name: (profile, sequences, lmin, lmax, seed, scaling)  -- SURVEY 8(d) / BASELINE.md
+    # weak: sequences per GPU; strong: sequences of the whole job, sharded over the GPUs
+    "cfg2": ("100.hmm", 10_000, 300, 500, 1, "weak"),
+    "cfg3": ("1400.hmm", 100_000, 300, 500, 2, "weak"),
+    "cfg4": ("1400.hmm", 1_000_000, 300, 500, 3, "strong"),
+    "cfg5": ("2405.hmm", 100_000, 1500, 2500, 4, "weak"),
 }
 METRIC = "M residues/sec (GCUPS) for profile M=1400 vs 100k seqs, 1/2/4/8 GPU"
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # 78.64 T fp32 lane-ops/s
@@ -53,21 +57,30 @@ def parse():
                     help="untimed steps; the MI355X clock ramps over the first ~10 launches (3.8 -> 3.0 ms)")
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or 16")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may run on")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-order", action="store_true", help="dequeue in input order (no longest-first sort)")
     return ap.parse_args()
 
 
-def cpu_threads(arg: int) -> int:
-    if arg > 0:
-        return arg
-    n = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+def host_cpus() -> dict:
+    """nproc (os.cpu_count) and the CPUs this process may run on (sched_getaffinity)."""
     try:
-        n = min(n, len(os.sched_getaffinity(0)))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None  # cgroup v2 CPU quota in CPUs ("max" = none)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+            quota = None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
         pass
-    return max(1, n)
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota}
+
+
+def cpu_threads(arg: int) -> int:
+    return arg if arg > 0 else max(1, host_cpus()["affinity_cpus"])
 
 
 def cpu_model() -> str:
@@ -133,6 +146,7 @@ def cpu_baseline(profile_path, codes, offsets, gpu_scores, target_s, threads):
         "value": residues / sec / 1e6,
         "unit": "M residues/s",
         "cores": threads,
+        **host_cpus(),
         "kind": kind,
         "sample": f"first {n} of {n_total} sequences of this rank's batch ({residues} residues), "
                   f"{sec:.2f} s on {threads} host threads, one MSV_HMM per thread",
@@ -197,20 +211,31 @@ def main():
     cdev = dev if backend == "nccl" else torch.device("cpu")  # where collective tensors live
 
     import hmm_fasta_viterbi_amd as msv
+    from hmm_fasta_viterbi_amd import distributed
     from hmm_fasta_viterbi_amd.synthetic import random_batch
 
-    prof_name, n, lmin, lmax, seed = CONFIGS[args.config]
+    prof_name, n_cfg, lmin, lmax, seed, scaling = CONFIGS[args.config]
     prof_path = os.path.join(ROOT, "data", "profile_HMMs", prof_name)
     engine = msv.MSV_HMM(msv.Profile_HMM(prof_path), device=local)
     leng = engine.model_length - 1
     info = engine.describe()
 
-    codes, offsets = random_batch(seed * 1000 + rank, n, lmin, lmax)
+    if scaling == "weak":  # every rank its own batch of the config's size
+        codes, offsets = random_batch(seed * 1000 + rank, n_cfg, lmin, lmax)
+        first, width = 0, n_cfg
+    else:  # one job-wide set, residue-balanced contiguous shards (the same cut as msv_shard_bounds)
+        all_codes, all_offsets = random_batch(seed, n_cfg, lmin, lmax)
+        codes, offsets, first, last = distributed.shard(all_codes, all_offsets, world, rank)
+        bounds = [distributed.shard_bounds(all_offsets, world, r) for r in range(world)]
+        width = max(b - a for a, b in bounds)  # gather pads every shard to the largest
+        del all_codes
+    n = len(offsets) - 1
     residues = int(offsets[-1])
     d_res = torch.from_numpy(codes).to(dev)
     d_off = torch.from_numpy(offsets.view(np.int64)).to(dev)
-    d_scores = torch.empty(n, dtype=torch.float32, device=dev)
-    d_order = torch.empty(n, dtype=torch.int32, device=dev)
+    d_scores = torch.full((max(width, 1),), float("nan"), dtype=torch.float32, device=dev)
+    d_order = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    gathered = torch.empty(world * max(width, 1), dtype=torch.float32, device=cdev) if scaling == "strong" else None
     # A dedicated stream: torch's default (null) stream has handle 0, which the C-ABI reads as
     # "use the library's own stream"; events must be recorded on the stream the kernel runs on.
     stream = torch.cuda.Stream(dev)
@@ -228,6 +253,26 @@ def main():
         engine.score_batch_device(d_res.data_ptr(), residues, d_off.data_ptr(), n, d_scores.data_ptr(), order_ptr, sh)
         if ev is not None:
             ev[1].record(stream)
+        if gathered is not None and world > 1:  # cfg4: the RCCL gather of the scores is part of the step
+            with torch.cuda.stream(stream):
+                src = d_scores if backend == "nccl" else d_scores.cpu()
+                dist.all_gather_into_tensor(gathered, src)
+
+    # Informational end-to-end rates first (their calls also bring the GPU clock up before the timed
+    # loop): host buffers -> msv_score_batch (H2D pipelined under the kernels, scores D2H), warm.
+    # Pinned = residues in page-locked memory (SURVEY 8(d)'s headline shape); pageable = plain numpy.
+    pinned_codes = torch.from_numpy(codes).pin_memory().numpy()
+
+    def host_rate(src):
+        for _ in range(3):
+            engine.score_batch(codes=src, offsets=offsets)
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            out = engine.score_batch(codes=src, offsets=offsets)
+        return residues * args.steps / (time.perf_counter() - t) / 1e6, out
+
+    host_pinned, pinned_scores = host_rate(pinned_codes)
+    host_pageable, pageable_scores = host_rate(codes)
 
     for _ in range(args.warmup):
         step()
@@ -254,55 +299,27 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), float(t[1])
         r = torch.tensor([residues], dtype=torch.int64, device=cdev)
-        dist.all_reduce(r, op=dist.ReduceOp.SUM)  # ranks draw different batches (seed + rank)
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
         residues_all = int(r[0])
 
-    # Output collection (outside the timed region): RCCL all-gather of every rank's scores.
+    # weak configs: output collection after timing (RCCL all-gather of every rank's scores)
     gather_ms = None
-    if world > 1:
+    if world > 1 and gathered is None:
         torch.cuda.synchronize(dev)
         g0 = time.perf_counter()
         full = torch.empty(world * n, dtype=torch.float32, device=cdev)
-        dist.all_gather_into_tensor(full, d_scores.to(cdev))
+        dist.all_gather_into_tensor(full, d_scores[:n].to(cdev))
         torch.cuda.synchronize(dev)
         gather_ms = (time.perf_counter() - g0) * 1e3
 
-    scores = d_scores.cpu().numpy()
+    scores = d_scores[:n].cpu().numpy()
     ok = bool(np.all(np.isfinite(scores)))
-    # Informational (SURVEY 8(d) "headline" in the survey's terms, never `value` here): packed residues
-    # in PINNED host memory -> H2D + order + kernel + D2H of the scores, on the same stream.
-    h_res = torch.from_numpy(codes).pin_memory()
-    h_off = torch.from_numpy(offsets.view(np.int64)).pin_memory()
-    h_sc = torch.empty(n, dtype=torch.float32).pin_memory()
-
-    def host_step():
-        with torch.cuda.stream(stream):
-            d_res.copy_(h_res, non_blocking=True)
-            d_off.copy_(h_off, non_blocking=True)
-        step()
-        with torch.cuda.stream(stream):
-            h_sc.copy_(d_scores, non_blocking=True)
-
-    host_step()
-    stream.synchronize()
-    t_p = time.perf_counter()
-    for _ in range(3):
-        host_step()
-    stream.synchronize()
-    pinned_s = (time.perf_counter() - t_p) / 3
-    ok_pinned = bool(np.array_equal(h_sc.numpy().view(np.uint32), d_scores.cpu().numpy().view(np.uint32)))
-
-    # Informational: the host-buffer C-ABI path (pageable H2D copy + kernel + D2H), i.e. the
-    # PCIe-inclusive rate; never the headline value.
-    host_scores = engine.score_batch(codes=codes, offsets=offsets)  # first call allocates its staging
-    host_api_s = 1e30
-    for _ in range(2):
-        t_h = time.perf_counter()
-        host_scores = engine.score_batch(codes=codes, offsets=offsets)
-        host_api_s = min(host_api_s, time.perf_counter() - t_h)
-    ok = ok and ok_pinned and bool(np.array_equal(host_scores.view(np.uint32), scores.view(np.uint32)))
-    total_residues = residues_all
-    value = total_residues * args.steps / elapsed / 1e6  # M residues / s, whole job
+    ok = ok and bool(np.array_equal(pinned_scores.view(np.uint32), scores.view(np.uint32)))
+    ok = ok and bool(np.array_equal(pageable_scores.view(np.uint32), scores.view(np.uint32)))
+    if gathered is not None and world > 1:  # every shard landed at its rows of the gathered set
+        g = gathered.cpu().numpy().reshape(world, -1)
+        ok = ok and bool(np.array_equal(g[rank, :n].view(np.uint32), scores.view(np.uint32)))
+    value = residues_all * args.steps / elapsed / 1e6  # M residues / s, whole job
     gcups = value * 1e6 * leng / 1e9
 
     result = None
@@ -312,6 +329,7 @@ def main():
         alg_bytes = residues + n * (8 + 8 + 4 + 4) + 21 * info["lanes_per_group"] * info["states_per_lane"] * 4
         traffic = pmc_traffic(args.config)
         ceiling = issue_ceiling_tcells()
+        per = "per GPU" if scaling == "weak" else f"in one set, {world} residue-balanced shard(s)"
         result = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -321,18 +339,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: seeded uniform residues (random_FASTA_generator.py format), lengths uniform "
                     f"[{lmin},{lmax}]; real Pfam profile {prof_name}",
             "config": {
-                "workload": f"{args.config}: {prof_name} (LENG={leng}) x {n} sequences per GPU, len U[{lmin},{lmax}], "
-                            "inputs resident in HBM",
+                "workload": f"{args.config}: {prof_name} (LENG={leng}) x {n_cfg} sequences {per}, "
+                            f"len U[{lmin},{lmax}], inputs resident in HBM",
                 "profile": prof_name,
-                "sequences_per_gpu": n,
-                "residues_per_gpu": residues,
-                "parallelism": f"dp{world} (sequence shards, no data-path collective)",
+                "sequences_rank0": n,
+                "residues_rank0": residues,
+                "residues_all_ranks": residues_all,
+                "parallelism": f"dp{world} (sequence shards, no data-path collective"
+                               + ("; RCCL all-gather of the scores in every step)" if scaling == "strong" else ")"),
                 "kernel_variant": info["variant"],
                 "dequeue_order": "input" if args.no_order else "longest-first",
             },
@@ -346,7 +366,8 @@ def main():
                 "frac": round(achieved / VALU_PEAK_TOPS, 4),
                 "traffic": traffic,
                 "note": "fp32 add/max ops: 3 per DP cell (cells = residues x LENG); peak = 256 CU x 128 "
-                        "lanes/clk x 2.4 GHz non-FMA VALU; HBM is not the bound (see hbm)",
+                        "lanes/clk x 2.4 GHz non-FMA VALU; HBM is not the bound (see hbm); traffic = "
+                        "calibrated FETCH_SIZE + WRITE_SIZE per launch (profiles/pmc_<config>.json)",
             },
             "issue_ceiling": None if ceiling is None else {
                 "tcells_per_s": round(ceiling, 3),
@@ -362,9 +383,16 @@ def main():
                 "peak_GBps": HBM_PEAK_GBPS,
             },
             "gather_ms": gather_ms,
-            "host_api_M_residues_s": round(residues / host_api_s / 1e6, 1),
-            "host_pinned_M_residues_s": round(residues / pinned_s / 1e6, 1),
-            "scores_finite": ok,
+            "end_to_end": {
+                "host_pinned_M_residues_s": round(host_pinned, 1),
+                "host_pageable_M_residues_s": round(host_pageable, 1),
+                "pinned_frac_of_value": round(host_pinned / (residues * args.steps / elapsed / 1e6), 4),
+                "note": "SURVEY 8(d)'s 'GPU timing' headline is host_pinned (packed residues in pinned host "
+                        "memory -> msv_score_batch: H2D pipelined under the kernels, order, kernels, scores "
+                        "D2H; rank 0, warm, mean of `steps` calls); `value` is the HBM-resident rate the "
+                        "bench contract prescribes",
+            },
+            "scores_finite_and_consistent": ok,
         }
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(prof_path, codes, offsets, scores, args.cpu_seconds,

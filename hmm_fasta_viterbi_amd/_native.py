@@ -44,7 +44,7 @@ EXPORTED = [
     "msv_fasta_parse_device", "msv_fasta_read_device", "msv_fasta_device_destroy", "msv_fasta_device_count",
     "msv_fasta_device_rejected", "msv_fasta_device_residues", "msv_fasta_device_codes", "msv_fasta_device_offsets",
     "msv_fasta_device_header_spans", "msv_fasta_device_text", "msv_fasta_device_download",
-    "msv_fasta_device_max_length", "msv_score_fasta_device",
+    "msv_fasta_device_max_length", "msv_score_fasta_device", "msv_fasta_device_device",
 ]
 
 
@@ -67,11 +67,15 @@ class KernelInfo(C.Structure):
         ("max_length", C.c_uint32),
         ("device", C.c_int),
         ("variant", C.c_char * 64),
+        ("latency_variant", C.c_char * 64),
+        ("latency_blocks", C.c_uint32),
+        ("latency_max_n", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
         d = {f: getattr(self, f) for f, _ in self._fields_}
         d["variant"] = self.variant.decode()
+        d["latency_variant"] = self.latency_variant.decode()
         return d
 
 
@@ -138,6 +142,7 @@ def lib() -> C.CDLL:
         "msv_fasta_read_device": (C.c_int, [C.c_int, C.c_char_p, vp, vp]),
         "msv_fasta_device_destroy": (None, [vp]),
         "msv_fasta_device_count": (u64, [vp]),
+        "msv_fasta_device_device": (C.c_int, [vp]),
         "msv_fasta_device_rejected": (u64, [vp]),
         "msv_fasta_device_residues": (u64, [vp]),
         "msv_fasta_device_codes": (vp, [vp]),

@@ -747,6 +747,7 @@ msv_status msv_fasta_device_download(const msv_fasta_device* f, uint8_t* codes, 
 }
 
 uint64_t msv_fasta_device_count(const msv_fasta_device* f) { return f ? f->count : 0; }
+int msv_fasta_device_device(const msv_fasta_device* f) { return f ? f->device : -1; }
 uint64_t msv_fasta_device_rejected(const msv_fasta_device* f) { return f ? f->rejected : 0; }
 uint64_t msv_fasta_device_residues(const msv_fasta_device* f) { return f ? f->residues : 0; }
 uint64_t msv_fasta_device_max_length(const msv_fasta_device* f) { return f ? f->max_length : 0; }

@@ -10,6 +10,9 @@
  * Ownership: the caller owns every buffer it passes; the library owns the device buffers held
  * by an msv_profile.  One msv_profile may be used by one host thread at a time (the reference
  * MSV_HMM is likewise not thread-safe, MSV_HMM.hpp:33-34); separate profiles are independent.
+ * From that one thread, a profile's device launches may go to any streams: every launch takes
+ * its own dequeue counter (one of 8 slots, reused only after the slot's previous launch), so
+ * launches of one profile on different streams may overlap.
  *
  * Residues cross the boundary as codes 0..19 in the reference's alphabetical order
  * A C D E F G H I K L M N P Q R S T V W Y (MSV_HMM.cpp:29-31), without the '#' sentinel that
@@ -105,6 +108,7 @@ msv_status msv_fasta_parse_device(int device, const uint8_t* d_text, uint64_t n,
 msv_status msv_fasta_read_device(int device, const char* path, void* stream, msv_fasta_device** out);
 void msv_fasta_device_destroy(msv_fasta_device* fasta);
 uint64_t msv_fasta_device_count(const msv_fasta_device* fasta);
+int msv_fasta_device_device(const msv_fasta_device* fasta);           /* the GPU holding it, -1 for NULL */
 uint64_t msv_fasta_device_rejected(const msv_fasta_device* fasta);
 uint64_t msv_fasta_device_residues(const msv_fasta_device* fasta);
 uint64_t msv_fasta_device_max_length(const msv_fasta_device* fasta);  /* longest record */
@@ -143,7 +147,10 @@ typedef struct msv_kernel_info {
     uint32_t blocks;           /* workgroups per launch (persistent grid)            */
     uint32_t max_length;       /* longest sequence the transition table covers        */
     int device;
-    char variant[64];
+    char variant[64];          /* throughput plan: every batch above latency_max_n sequences */
+    char latency_variant[64];  /* small-batch plan (one sequence per wave), "" if none      */
+    uint32_t latency_blocks;   /* its persistent grid                                    */
+    uint64_t latency_max_n;    /* batches of up to this many sequences take it            */
 } msv_kernel_info;
 msv_status msv_profile_describe(const msv_profile* profile, msv_kernel_info* out);
 
@@ -161,7 +168,9 @@ msv_status msv_profile_reserve_length(msv_profile* profile, uint64_t max_length)
 /* Host buffers in, host scores out; synchronous.  n = number of sequences; offsets has n+1
  * entries, offsets[0] may be non-zero.  scores[s] = MSV log-odds score of sequence s, exactly
  * MSV_HMM::run_on_sequence (MSV_HMM.cpp:74-113); an empty sequence scores -inf.
- * stream may be NULL (the library's own stream). */
+ * stream may be NULL (the library's own stream).  Batches of >= 4 Mi residues run as a copy/compute
+ * pipeline (H2D of later pieces under the kernels of earlier ones); residues in pinned host memory
+ * (hipHostMalloc, torch pin_memory) copy at full PCIe rate without runtime staging. */
 msv_status msv_score_batch(msv_profile* profile, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
                            float* scores, void* stream);
 
@@ -184,7 +193,8 @@ msv_status msv_order_longest_first(msv_profile* profile, const uint64_t* d_offse
                                    void* stream);
 
 /* A GPU-parsed FASTA set (msv_fasta_read_device) scored in place: length table reserved for its
- * longest record, longest-first order, one launch, scores copied to the host (count() floats). */
+ * longest record, longest-first order, one launch, scores copied to the host (count() floats).
+ * The set must live on the profile's device (else MSV_ERR_INVALID_ARGUMENT). */
 msv_status msv_score_fasta_device(msv_profile* profile, const msv_fasta_device* fasta, float* scores);
 
 /* ---- profiles x sequences grid ---------------------------------------------
@@ -213,7 +223,8 @@ msv_status msv_shard_bounds(const uint64_t* offsets, uint64_t n, uint32_t n_shar
 /* profiles[k]: the same model created on device k (msv_profile_create_from_hmm(k, ...)).  Shard k
  * of the batch is scored on profiles[k]'s device by its own host thread (upload, longest-first
  * order, one launch, download), all shards concurrently; scores land in input order.  The same
- * device may appear more than once (its shards then share the GPU). */
+ * device may appear more than once (its shards then share the GPU); the same HANDLE may too, and
+ * then scores its shards one after another on one thread. */
 msv_status msv_score_batch_multi(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* residues,
                                  const uint64_t* offsets, uint64_t n, float* scores);
 

@@ -9,8 +9,10 @@
 //   * errors throw (msv_error, or std::out_of_range for a residue outside the 20 amino acids,
 //     exactly what the reference's amino_acid_num.at throws, MSV_HMM.cpp:101) instead of printing
 //     and continuing with a half-built object (Profile_HMM.cpp:50-53, MSV_HMM.cpp:198-203);
-//   * run_on_sequence and parallel_run_on_sequence both score on the GPU (bit-identical to the
-//     reference CPU DP); the reference's sequential CPU DP lives only in oracle/ as the checker;
+//   * run_on_sequence is, as in the reference, the sequential CPU DP (this library's own
+//     restatement, two rolling rows); parallel_run_on_sequence and score_batch* score on the GPU.
+//     Both are bit-identical to the reference's CPU DP, so the reference's seq-vs-par differential
+//     (test_MSV.cpp:23-26) compares CPU and GPU;
 //   * score_batch adds the batch API the reference lacks: one kernel launch per batch.
 #pragma once
 
@@ -101,7 +103,8 @@ class MSV_HMM {
     MSV_HMM(MSV_HMM&& o) noexcept;
     MSV_HMM& operator=(MSV_HMM&& o) noexcept;
 
-    // One sequence ('#' + residues).  Scored by the same fused kernel as a batch of one.
+    // One sequence ('#' + residues).  run_on_sequence: the sequential CPU DP (MSV_HMM.cpp:74-113);
+    // parallel_run_on_sequence: the fused gfx950 kernel, as a batch of one (MSV_HMM.cpp:269-430).
     Log_score run_on_sequence(const Protein_sequence& seq);
     Log_score parallel_run_on_sequence(const Protein_sequence& seq, bool should_specialize = false);
 

@@ -1,9 +1,11 @@
 // test_msv.cpp -- GPU parity driver in the shape of the reference's differential test
 // (algorithms/test_MSV.cpp:14-36): every profile x fasta_like_example.fsa, scored through
-// run_on_sequence, parallel_run_on_sequence(seq) and parallel_run_on_sequence(seq, true),
-// plus the batch API.  Unlike the reference (which only checks seq vs par within 1e-4,
-// test_MSV.cpp:10-12,26), every score is compared BITWISE with the golden scores the
-// reference's own CPU path produced (tests/golden/example_scores.tsv, oracle/make_golden.py).
+// run_on_sequence (the CPU DP), parallel_run_on_sequence(seq) and parallel_run_on_sequence(seq,
+// true) (the GPU kernel), plus the batch API.  Unlike the reference (which only checks seq vs par
+// within 1e-4, test_MSV.cpp:10-12,26), every score is compared BITWISE with the golden scores the
+// reference's own CPU path produced (tests/golden/example_scores.tsv, oracle/make_golden.py), and
+// the seq-vs-par differential itself (CPU vs GPU) runs bitwise on seeded sequences for every
+// profile.
 // Usage: test_msv <repo_root>   (exit 0 = pass)
 #include <cmath>
 #include <cstdio>
@@ -91,6 +93,38 @@ int main(int argc, char** argv) {
             }
         }
     }
+    // the reference's seq-vs-par differential (test_MSV.cpp:23-26), bitwise: the CPU DP against the
+    // GPU kernel on seeded sequences of lengths 0..700 for every profile (one GPU batch per profile)
+    {
+        uint64_t x = 0x9E3779B97F4A7C15ull;
+        auto next = [&] {
+            x ^= x << 13;
+            x ^= x >> 7;
+            x ^= x << 17;
+            return x;
+        };
+        const char* letters = "ACDEFGHIKLMNPQRSTVWY";
+        Protein_sequences seqs;
+        for (int i = 0; i < 40; ++i) {
+            std::string s = "#";
+            const size_t L = i < 3 ? static_cast<size_t>(i) : next() % 701;
+            for (size_t k = 0; k < L; ++k) s += letters[next() % 20];
+            seqs.push_back(s);
+        }
+        for (const auto& kv : golden) {
+            auto m = MSV_HMM(Profile_HMM(root + "/data/profile_HMMs/" + kv.first));
+            auto par = m.score_batch(seqs);
+            for (size_t i = 0; i < seqs.size(); ++i) {
+                const float seq = m.run_on_sequence(seqs[i]);
+                if (!same_bits(seq, par[i])) {
+                    std::printf("test_msv failed! seq vs par %s random seq %zu (L=%zu): cpu %a, gpu %a\n",
+                                kv.first.c_str(), i, seqs[i].size() - 1, seq, par[i]);
+                    return 1;
+                }
+                ++checked;
+            }
+        }
+    }
     // error behaviour: a residue outside the 20 throws std::out_of_range like amino_acid_num.at
     auto msv = MSV_HMM(Profile_HMM(root + "/data/profile_HMMs/100.hmm"));
     bool threw = false;
@@ -99,11 +133,17 @@ int main(int argc, char** argv) {
     } catch (const std::out_of_range&) {
         threw = true;
     }
+    try {
+        msv.parallel_run_on_sequence("#ACDXEF");
+        threw = false;
+    } catch (const std::out_of_range&) {
+    }
     if (!threw) {
         std::printf("test_msv failed! bad residue did not throw\n");
         return 1;
     }
-    if (!std::isinf(msv.run_on_sequence("#")) || msv.run_on_sequence("#") > 0) {
+    if (!std::isinf(msv.run_on_sequence("#")) || msv.run_on_sequence("#") > 0 ||
+        !std::isinf(msv.parallel_run_on_sequence("#")) || msv.parallel_run_on_sequence("#") > 0) {
         std::printf("test_msv failed! empty sequence must score -inf\n");
         return 1;
     }

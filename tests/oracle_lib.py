@@ -84,13 +84,27 @@ class OracleProfile:
     def name(self) -> str:
         return self.L.oracle_profile_name(self.p).decode()
 
-    def score_batch(self, codes: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+    def score_batch(self, codes: np.ndarray, offsets: np.ndarray, threads: int = 1) -> np.ndarray:
+        """Oracle scores of a CSR batch; `threads` > 1 splits the sequences over host threads (the
+        oracle profile is read-only, and ctypes releases the GIL during each call)."""
         codes = np.ascontiguousarray(codes, np.uint8)
         offsets = np.ascontiguousarray(offsets, np.uint64)
         n = len(offsets) - 1
         out = np.zeros(n, np.float32)
-        self.L.oracle_profile_score_batch(self.p, codes.ctypes.data if codes.size else None, offsets.ctypes.data, n,
-                                          out.ctypes.data)
+        base = codes.ctypes.data if codes.size else None
+
+        def run(lo, hi):
+            if hi > lo:
+                self.L.oracle_profile_score_batch(self.p, base, offsets[lo:].ctypes.data, hi - lo,
+                                                  out[lo:].ctypes.data)
+
+        if threads <= 1 or n < 2 * threads:
+            run(0, n)
+            return out
+        from concurrent.futures import ThreadPoolExecutor
+        cuts = np.linspace(0, n, threads + 1).astype(np.int64)
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(lambda k: run(int(cuts[k]), int(cuts[k + 1])), range(threads)))
         return out
 
     def score_string(self, seq: str) -> float:

@@ -92,3 +92,4 @@ def test_host_only_entry_points_validate_arguments():
     assert L.msv_fasta_read_device(0, None, None, C.byref(f)) == 1
     assert L.msv_fasta_device_count(None) == 0 and L.msv_fasta_device_codes(None) is None
     assert L.msv_score_fasta_device(None, None, None) == 1
+    assert L.msv_fasta_device_device(None) == -1  # no set: no device

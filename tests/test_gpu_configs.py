@@ -1,0 +1,195 @@
+"""BASELINE.json's configs at full size on the GPU, the host-buffer pipeline, and the per-launch
+counter slots.  Bitwise against the oracle (tests/oracle_lib.py) on samples, and through
+size-independent properties (three scorings agree, determinism, permutation invariance) on the
+whole batch.
+
+  cfg4: 1400.hmm x 1,000,000 sequences, len U[300,500], seed 3 -- one launch, the host pipeline,
+        8 residue-balanced shards through msv_score_batch_multi (the one device listed 8 times) and
+        distributed.shard slices must all give the same bits; >= 256 oracle samples incl. the
+        longest and shortest sequences.
+  cfg5: 2405.hmm x 100,000 sequences, len U[1500,2500], seed 4 -- determinism, permutation
+        invariance, >= 500 oracle samples incl. the longest and shortest sequences.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import hmm_fasta_viterbi_amd as msv
+from hmm_fasta_viterbi_amd import distributed
+from hmm_fasta_viterbi_amd.synthetic import concat_batches, homolog_batch, random_batch
+from oracle_lib import OracleProfile, bits, profile_path
+
+ORACLE_THREADS = min(16, len(os.sched_getaffinity(0)))
+
+
+def subset(codes, offsets, idx):
+    parts = [codes[int(offsets[i]):int(offsets[i + 1])] for i in idx]
+    offs = np.zeros(len(idx) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(p) for p in parts])
+    return (np.concatenate(parts) if parts else np.zeros(0, np.uint8)), offs
+
+
+def sample_with_extremes(offsets, k, seed):
+    """k sequence indices: the longest, the shortest, the first and last, and a seeded spread."""
+    lens = np.diff(offsets.astype(np.int64))
+    n = len(lens)
+    pick = {int(np.argmax(lens)), int(np.argmin(lens)), 0, n - 1}
+    rng = np.random.default_rng(seed)
+    pick.update(int(i) for i in rng.choice(n, k, replace=False))
+    return np.array(sorted(pick), np.int64)
+
+
+def device_scores(engine, codes, offsets, order=True):
+    """One launch over the whole batch resident in HBM (torch tensors, caller stream)."""
+    import torch
+    dev = torch.device("cuda", engine.device)
+    n = len(offsets) - 1
+    r = torch.from_numpy(codes).to(dev)
+    o = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    s = torch.full((n,), float("nan"), dtype=torch.float32, device=dev)
+    st = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    engine.reserve_length(int(np.diff(offsets.astype(np.int64)).max()))
+    ordp = None
+    if order:
+        ordt = torch.empty(n, dtype=torch.int32, device=dev)
+        engine.order_longest_first(o.data_ptr(), n, ordt.data_ptr(), st.cuda_stream)
+        ordp = ordt.data_ptr()
+    engine.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), n, s.data_ptr(), ordp, st.cuda_stream)
+    engine.check(st.cuda_stream)
+    return s.cpu().numpy()
+
+
+def test_cfg4_full_size_three_ways():
+    prof = msv.Profile_HMM(profile_path("1400.hmm"))
+    e = msv.MSV_HMM(prof)
+    codes, offsets = random_batch(3, 1_000_000, 300, 500)
+    assert int(offsets[-1]) < (1 << 32)
+    one = device_scores(e, codes, offsets)                      # (a) one launch
+    assert np.all(np.isfinite(one))
+    host = e.score_batch(codes=codes, offsets=offsets)           # the host-buffer pipeline (pieces)
+    assert np.array_equal(bits(host), bits(one))
+    engines = [msv.MSV_HMM(prof, device=0) for _ in range(8)]    # (b) 8 shards, msv_score_batch_multi
+    multi = msv.score_batch_multi(engines, codes=codes, offsets=offsets)
+    assert np.array_equal(bits(multi), bits(one))
+    bounds = msv.shard_bounds(offsets, 8)                        # (c) the torch.distributed split
+    sliced = np.empty_like(one)
+    for r in range(8):
+        c, o, first, last = distributed.shard(codes, offsets, 8, r)
+        assert (first, last) == (int(bounds[r]), int(bounds[r + 1]))
+        sliced[first:last] = e.score_batch(codes=c, offsets=o)
+    assert np.array_equal(bits(sliced), bits(one))
+    # residue balance of the shards (BASELINE cfg4's 8-GPU split)
+    res = np.diff(offsets[bounds.astype(np.int64)].astype(np.int64))
+    assert res.max() - res.min() <= 2 * 500
+    idx = sample_with_extremes(offsets, 256, 4)
+    want = OracleProfile("1400").score_batch(*subset(codes, offsets, idx), threads=ORACLE_THREADS)
+    assert np.array_equal(bits(one[idx]), bits(want))
+    for x in engines:
+        x.close()
+    e.close()
+
+
+def test_cfg5_full_size_properties():
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("2405.hmm")))
+    codes, offsets = random_batch(4, 100_000, 1500, 2500)
+    a = e.score_batch(codes=codes, offsets=offsets)
+    b = device_scores(e, codes, offsets)
+    assert np.array_equal(bits(a), bits(b))
+    assert np.all(np.isfinite(a))
+    perm = np.random.default_rng(1).permutation(100_000)[:5000]
+    pc, po = subset(codes, offsets, perm)
+    assert np.array_equal(bits(e.score_batch(codes=pc, offsets=po)), bits(a[perm]))
+    idx = sample_with_extremes(offsets, 500, 5)
+    want = OracleProfile("2405").score_batch(*subset(codes, offsets, idx), threads=ORACLE_THREADS)
+    assert np.array_equal(bits(a[idx]), bits(want))
+    e.close()
+
+
+def test_host_pipeline_piece_edges():
+    """msv_score_batch over >= 4 Mi residues runs as pieces on two compute streams + a copy stream:
+    empty records, a long record and homologs placed around the piece cuts; pinned (torch
+    pin_memory) and pageable sources; equal to one device launch."""
+    import torch
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("700.hmm")))
+    rc, ro = random_batch(201, 12_000, 0, 900)
+    hc, ho = homolog_batch(msv.Profile_HMM(profile_path("700.hmm")).match_emissions, 202, 400, 1, 900)
+    long = np.random.default_rng(3).integers(0, 20, 150_000, dtype=np.uint8)
+    lc, lo = long, np.array([0, long.size], np.uint64)
+    empty = (np.zeros(0, np.uint8), np.zeros(2001, np.uint64))
+    codes, offsets = concat_batches((rc, ro), empty, (lc, lo), (hc, ho), (rc, ro), empty)
+    assert int(offsets[-1]) >= 4 << 20
+    want = device_scores(e, codes, offsets)
+    got = e.score_batch(codes=codes, offsets=offsets)
+    assert np.array_equal(bits(got), bits(want))
+    pc = torch.from_numpy(codes).pin_memory()
+    po = torch.from_numpy(offsets.view(np.int64)).pin_memory()
+    got = e.score_batch(codes=pc.numpy(), offsets=po.numpy().view(np.uint64))
+    assert np.array_equal(bits(got), bits(want))
+    idx = sample_with_extremes(offsets, 60, 7)
+    assert np.array_equal(bits(want[idx]), bits(OracleProfile("700").score_batch(*subset(codes, offsets, idx),
+                                                                                  threads=ORACLE_THREADS)))
+    # an offsets array that does not start at 0 (a slice of a larger batch)
+    sub = e.score_batch(codes=codes, offsets=offsets[5000:])
+    assert np.array_equal(bits(sub), bits(want[5000:]))
+    e.close()
+
+
+def test_one_profile_on_two_streams_without_sync():
+    """launches of one profile on different streams with no synchronisation between them
+    (a device call on a torch stream, then the host API on the library's stream, then two more
+    device calls on two other streams) each take their own dequeue counter slot."""
+    import torch
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("1400.hmm")))
+    dev = torch.device("cuda:0")
+    batches = [random_batch(300 + k, n, 0, 700) for k, n in enumerate((70_000, 20_000, 50_000, 9_000))]
+    e.reserve_length(700)
+    ref = [e.score_batch(codes=c, offsets=o) for c, o in batches]
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    tens = []
+    for c, o in batches:
+        tens.append((torch.from_numpy(c).to(dev), torch.from_numpy(o.view(np.int64)).to(dev),
+                     torch.full((len(o) - 1,), float("nan"), dtype=torch.float32, device=dev)))
+    torch.cuda.synchronize()
+    for rep in range(3):
+        r, o, s = tens[0]
+        e.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), s.numel(), s.data_ptr(), None,
+                             streams[0].cuda_stream)
+        host = e.score_batch(codes=batches[1][0], offsets=batches[1][1])  # library stream, no sync first
+        for k in (2, 3):
+            r, o, s = tens[k]
+            e.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), s.numel(), s.data_ptr(), None,
+                                 streams[k - 1].cuda_stream)
+        torch.cuda.synchronize()
+        e.check()
+        assert np.array_equal(bits(host), bits(ref[1])), rep
+        for k in (0, 2, 3):
+            assert np.array_equal(bits(tens[k][2].cpu().numpy()), bits(ref[k])), (rep, k)
+    e.close()
+
+
+def test_score_batch_multi_same_handle_twice():
+    """the same profile handle listed more than once scores its shards one after another
+    on one host thread (no race on its staging buffers)."""
+    prof = msv.Profile_HMM(profile_path("1400.hmm"))
+    a, b = msv.MSV_HMM(prof), msv.MSV_HMM(prof)
+    codes, offsets = random_batch(72, 30_000, 0, 800)
+    want = a.score_batch(codes=codes, offsets=offsets)
+    for handles in ([a, a], [a, b, a, b, a], [b, b, b, b]):
+        got = msv.score_batch_multi(handles, codes=codes, offsets=offsets)
+        assert np.array_equal(bits(got), bits(want)), len(handles)
+    a.close()
+    b.close()
+
+
+def test_describe_reports_both_plans():
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("1400.hmm")))
+    d = e.describe()
+    assert d["latency_variant"].startswith("msv_g64_") and d["latency_max_n"] >= 4096
+    assert d["latency_blocks"] > 0 and d["variant"] != d["latency_variant"]
+    small = msv.MSV_HMM(msv.Profile_HMM(profile_path("100.hmm"))).describe()
+    assert small["latency_variant"] == "" and small["latency_max_n"] == 0
+    e.close()

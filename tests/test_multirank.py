@@ -7,6 +7,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 from hmm_fasta_viterbi_amd.distributed import shard, shard_bounds
 from hmm_fasta_viterbi_amd.synthetic import random_batch
@@ -70,3 +71,41 @@ def test_gloo_world_size_2(tmp_path):
     outs = [p.communicate(timeout=300)[0] for p in procs]
     assert all(p.returncode == 0 for p in procs), outs
     assert "MULTIRANK_OK" in outs[0]
+
+
+GPU_WORKER = r'''
+import os, sys
+sys.path.insert(0, {root!r}); sys.path.insert(0, os.path.join({root!r}, "tests"))
+import numpy as np, torch.distributed as dist
+import hmm_fasta_viterbi_amd as msv
+from hmm_fasta_viterbi_amd.distributed import score_sharded
+from hmm_fasta_viterbi_amd.synthetic import random_batch
+from oracle_lib import OracleProfile, profile_path
+dist.init_process_group("gloo")
+engine = msv.MSV_HMM(msv.Profile_HMM(profile_path("1400")), device=0)
+codes, offsets = random_batch(3, 40_000, 300, 500)  # the cfg4 shape (seed 3), 40k of its 1M
+got = score_sharded(engine.score_batch, codes, offsets)
+if dist.get_rank() == 0:
+    want = engine.score_batch(codes=codes, offsets=offsets)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    idx = np.arange(0, 40_000, 1999)
+    parts = [codes[int(offsets[i]):int(offsets[i + 1])] for i in idx]
+    o = np.zeros(len(idx) + 1, np.uint64); o[1:] = np.cumsum([len(p) for p in parts])
+    assert np.array_equal(got[idx].view(np.uint32), OracleProfile("1400").score_batch(np.concatenate(parts), o).view(np.uint32))
+    print("MULTIRANK_GPU_OK")
+dist.destroy_process_group()
+'''
+
+
+@pytest.mark.gpu
+def test_gloo_world_size_2_hip_scorer(tmp_path):
+    """The sharded path with the HIP scorer under a process group: 2 ranks on the one GPU of the box
+    (gloo for the gather), gathered scores bitwise equal to one process scoring everything."""
+    script = tmp_path / "gpu_worker.py"
+    script.write_text(GPU_WORKER.format(root=ROOT))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE="2")
+    procs = [subprocess.Popen([sys.executable, str(script)], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=180)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    assert "MULTIRANK_GPU_OK" in outs[0]

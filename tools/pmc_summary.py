@@ -1,9 +1,16 @@
 """Summarise tools/pmc.sh output for the msv_batch_kernel dispatches.
 
-HBM traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) KiB: on gfx950 FETCH_SIZE reports half the
-bytes of wide coalesced reads (MI355X_MICROARCH.md §HBM); our reads are narrow (1-byte residues,
-8-byte offsets), for which the factor is uncalibrated, so both the raw and the doubled figure are
-reported and the doubled one is used as the (upper-bound) traffic.
+HBM traffic per launch = factor * FETCH_SIZE + WRITE_SIZE.  On gfx950 FETCH_SIZE reports half the
+bytes of wide coalesced reads (MI355X_MICROARCH.md §HBM) and is uncalibrated for other widths; the
+MSV kernel's reads are dominated (~94% of its bytes) by the residue stream, 1-byte loads that 16
+lanes issue to one address, so `factor` is the one MEASURED for exactly that pattern by
+tools/micro/fetch_calib.hip (profiles/r02_fetch_calib.json, kernel k_ubyte_group); without that
+file the guide's factor 2 is used and the figure is flagged uncalibrated.
+
+VALU issue busy = SQ_INSTS_VALU x 2 cycles (a wave64 VALU instruction occupies a SIMD32 for 2
+cycles) / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8): GRBM_GUI_ACTIVE is summed over the 8 XCDs (its
+per-XCD value over the kernel time gives the clock).  This counts issue slots of full-rate
+instructions; v_max/v_max3 occupy about twice that (tools/micro/valu_rate.hip).
 """
 import csv
 import glob
@@ -39,12 +46,19 @@ def main():
         if "GRBM_GUI_ACTIVE" in avg:
             res["effective_clock_GHz"] = avg["GRBM_GUI_ACTIVE"] / 8 / t / 1e9 if avg["GRBM_GUI_ACTIVE"] > 1e6 else None
     if "FETCH_SIZE" in avg:
+        factor, calibrated = 2.0, False
+        cal = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "r02_fetch_calib.json")
+        if os.path.exists(cal):
+            with open(cal) as f:
+                factor = json.load(f)["kernels"]["k_ubyte_group"]["factor"]
+            calibrated = True
         res["fetch_kib_raw"] = avg["FETCH_SIZE"]
         res["write_kib"] = avg.get("WRITE_SIZE")
-        res["hbm_bytes_per_launch"] = int((2 * avg["FETCH_SIZE"] + avg.get("WRITE_SIZE", 0)) * 1024)
-    if "SQ_ACTIVE_INST_VALU" in avg and "GRBM_GUI_ACTIVE" in avg:
-        # VALUBusy as rocprofv3 defines it: SQ_ACTIVE_INST_VALU / CU_NUM / GRBM_GUI_ACTIVE
-        res["valu_busy_pct"] = 100 * avg["SQ_ACTIVE_INST_VALU"] / 256 / (avg["GRBM_GUI_ACTIVE"] / 8)
+        res["fetch_factor"] = factor
+        res["fetch_factor_calibrated"] = calibrated
+        res["hbm_bytes_per_launch"] = int((factor * avg["FETCH_SIZE"] + avg.get("WRITE_SIZE", 0)) * 1024)
+    if "SQ_INSTS_VALU" in avg and "GRBM_GUI_ACTIVE" in avg:
+        res["valu_issue_busy_pct"] = 100 * avg["SQ_INSTS_VALU"] * 2 / 1024 / (avg["GRBM_GUI_ACTIVE"] / 8)
     print(json.dumps(res, indent=1))
 
 
