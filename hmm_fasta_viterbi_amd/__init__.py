@@ -35,6 +35,13 @@ for _i, _c in enumerate(AMINO_ACIDS):
 _LUT[ord("#")] = 255
 
 
+def _loaded_lib():
+    """The loaded library, or None (also during interpreter shutdown, when module globals such as
+    `_native` may already be cleared before the last destructor runs)."""
+    native = globals().get("_native")
+    return getattr(native, "_lib", None) if native is not None else None
+
+
 def device_count() -> int:
     n = C.c_int(0)
     _native.lib().msv_device_count(C.byref(n))
@@ -96,8 +103,9 @@ class Profile_HMM:
         return es, b.value, c.value, j.value
 
     def __del__(self):
-        if getattr(self, "_h", None) and _native._lib is not None:
-            _native._lib.msv_hmm_destroy(self._h)
+        lib = _loaded_lib()
+        if getattr(self, "_h", None) and lib is not None:
+            lib.msv_hmm_destroy(self._h)
             self._h = None
 
 
@@ -249,8 +257,9 @@ class MSV_HMM:
         return info.as_dict()
 
     def close(self):
-        if getattr(self, "_p", None) and _native._lib is not None:
-            _native._lib.msv_profile_destroy(self._p)
+        lib = _loaded_lib()
+        if getattr(self, "_p", None) and lib is not None:
+            lib.msv_profile_destroy(self._p)
             self._p = None
 
     def __del__(self):
@@ -355,8 +364,9 @@ class FASTA_device:
         return codes, offsets, spans
 
     def close(self):
-        if getattr(self, "_f", None) and _native._lib is not None:
-            _native._lib.msv_fasta_device_destroy(self._f)
+        lib = _loaded_lib()
+        if getattr(self, "_f", None) and lib is not None:
+            lib.msv_fasta_device_destroy(self._f)
             self._f = None
 
     def __del__(self):

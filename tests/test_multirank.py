@@ -84,7 +84,7 @@ from oracle_lib import OracleProfile, profile_path
 dist.init_process_group("gloo")
 engine = msv.MSV_HMM(msv.Profile_HMM(profile_path("1400")), device=0)
 codes, offsets = random_batch(3, 40_000, 300, 500)  # the cfg4 shape (seed 3), 40k of its 1M
-got = score_sharded(engine.score_batch, codes, offsets)
+got = score_sharded(lambda c, o: engine.score_batch(codes=c, offsets=o), codes, offsets)
 if dist.get_rank() == 0:
     want = engine.score_batch(codes=codes, offsets=offsets)
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
