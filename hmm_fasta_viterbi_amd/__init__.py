@@ -156,6 +156,7 @@ class MSV_HMM:
         check(L.msv_profile_create(device, es.ctypes.data, self.model_length, self.tr_B_Mk, self.tr_E_C,
                                    self.tr_E_J, C.byref(p)), "msv_profile_create")
         self._p = p
+        self._inflight = {}  # msv_score_batch_async tickets -> the arrays the device still reads/writes
         self.device = device
         # STATS LOCAL MSV (Profile_HMM.cpp:83-85): parsed by the reference, used here for P-values
         self.msv_mu = base_hmm.stats_local_msv_mu
@@ -184,6 +185,33 @@ class MSV_HMM:
         if st == _native.MSV_ERR_BAD_RESIDUE:
             raise IndexError("residue outside the 20 amino acids")
         check(st, "msv_score_batch")
+        return out
+
+    def score_batch_async(self, codes: np.ndarray, offsets: np.ndarray, out: np.ndarray | None = None) -> int:
+        """Enqueue a host batch (msv_score_batch_async) and return a ticket; `wait(ticket)` returns
+        the scores.  At most two calls outstanding; pinned arrays (torch pin_memory().numpy()) make
+        the copies overlap the previous call's kernel.  The arrays are held until the wait."""
+        codes = np.ascontiguousarray(codes, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        n = len(offsets) - 1
+        if out is None:
+            out = np.zeros(n, np.float32)
+        if out.dtype != np.float32 or out.shape != (n,) or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous float32 array of n scores")
+        t = C.c_uint64(0)
+        check(_native.lib().msv_score_batch_async(self._p, codes.ctypes.data if codes.size else None,
+                                                  offsets.ctypes.data, n, out.ctypes.data, C.byref(t)),
+              "msv_score_batch_async")
+        self._inflight[t.value] = (codes, offsets, out)
+        return t.value
+
+    def wait(self, ticket: int) -> np.ndarray:
+        """Scores of an msv_score_batch_async call (raises its kernel-latched errors)."""
+        st = _native.lib().msv_profile_wait(self._p, ticket)
+        _, _, out = self._inflight.pop(ticket, (None, None, None))
+        if st == _native.MSV_ERR_BAD_RESIDUE:
+            raise IndexError("residue outside the 20 amino acids")
+        check(st, "msv_profile_wait")
         return out
 
     def score_batch_device(self, residues_ptr: int, residues_len: int, offsets_ptr: int, n: int, scores_ptr: int,

@@ -27,10 +27,12 @@ constexpr uint32_t kOrderBins = 4096;  // lengths >= 4095 share the longest bin
 // Every launch of one profile takes the next of kLaunchSlots device counter pairs {next index, waves
 // left} (and, for the longest-first order, the next histogram), so launches on different streams
 // never share a counter; a slot is reused only after its previous launch (an event wait when the
-// streams differ).  d_words: [2k, 2k+1] = slot k's counters, [kErrWord] = sticky error bits.
+// streams differ).  d_words: [2k, 2k+1] = slot k's counters, [kErrWord] = sticky error bits,
+// [kErrWord + 1 + a] = the error bits of asynchronous staging slot a (msv_score_batch_async).
 constexpr int kLaunchSlots = 8;
+constexpr int kAsyncSlots = 2;
 constexpr int kErrWord = 2 * kLaunchSlots;
-constexpr int kWords = kErrWord + 2;
+constexpr int kWords = kErrWord + 1 + kAsyncSlots + 1;
 // Every launch addresses < 2^32 residue bytes.
 constexpr uint64_t kChunkBytes = (1ull << 32) - (1ull << 20);
 // Host batches of at least this many residues are scored as a copy/compute pipeline of pieces.
@@ -201,6 +203,26 @@ struct msv_profile {
     std::vector<hipEvent_t> events;
     uint64_t* h_off = nullptr;
     size_t h_off_cap = 0;
+    uint32_t pipe_first_den = 16, pipe_growth = 2;  // piece sizes: total / first_den, then x growth
+    // msv_score_batch_async: kAsyncSlots staging sets, so the H2D of one call runs under the kernel
+    // of the call before it
+    struct AsyncSlot {
+        uint8_t* d_res = nullptr;
+        size_t res_cap = 0;
+        uint64_t* d_off = nullptr;
+        size_t off_cap = 0;
+        float* d_sc = nullptr;
+        size_t sc_cap = 0;
+        uint32_t* d_ord = nullptr;
+        size_t ord_cap = 0;
+        uint64_t* h_off = nullptr;  // pinned rebased offsets
+        size_t h_cap = 0;
+        uint32_t* h_err = nullptr;  // pinned copy of the slot's error word
+        hipEvent_t copied = nullptr, done = nullptr;
+        uint64_t ticket = 0;
+        bool pending = false;
+    } async[kAsyncSlots];
+    uint64_t next_ticket = 1;
     // host-API staging
     uint8_t* d_res = nullptr;
     size_t d_res_cap = 0;
@@ -311,10 +333,12 @@ static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
 // k's sequence range.  Each piece addresses < kChunkBytes residues and < 2^32 - 2^24 sequences (one
 // launch each).  Batches below kPipelineMin residues are one piece; larger ones start at ~1/16 of the
 // batch (at least 1M residues) and double, a short remainder joining the last piece.
-static std::vector<uint64_t> plan_pieces(const uint64_t* offsets, uint64_t n, uint64_t total) {
+static std::vector<uint64_t> plan_pieces(const uint64_t* offsets, uint64_t n, uint64_t total, uint32_t first_den,
+                                         uint32_t growth) {
     constexpr uint64_t kMaxSeqs = (1ull << 32) - (1ull << 24) - 1;
     std::vector<uint64_t> cut{0};
-    uint64_t want = total < kPipelineMin ? kChunkBytes : std::max<uint64_t>(1ull << 20, total / 16);
+    uint64_t want = (total < kPipelineMin || first_den == 0) ? kChunkBytes
+                                                             : std::max<uint64_t>(1ull << 20, total / first_den);
     uint64_t first = 0;
     while (first < n) {
         const uint64_t base = offsets[first];
@@ -329,7 +353,7 @@ static std::vector<uint64_t> plan_pieces(const uint64_t* offsets, uint64_t n, ui
         if (last < n && rest < want && offsets[n] - base < kChunkBytes && n - first <= kMaxSeqs) last = n;
         cut.push_back(last);
         first = last;
-        want = std::min(kChunkBytes, 2 * want);
+        want = std::min(kChunkBytes, std::max<uint32_t>(growth, 1) * want);
     }
     return cut;
 }
@@ -409,6 +433,16 @@ void msv_profile_destroy(msv_profile* p) {
     for (hipEvent_t e : p->events) (void)hipEventDestroy(e);
     p->kernels.destroy();
     p->orders.destroy();
+    for (auto& a : p->async) {
+        if (a.copied) (void)hipEventDestroy(a.copied);
+        if (a.done) (void)hipEventDestroy(a.done);
+        (void)hipFree(a.d_res);
+        (void)hipFree(a.d_off);
+        (void)hipFree(a.d_sc);
+        (void)hipFree(a.d_ord);
+        if (a.h_off) (void)hipHostFree(a.h_off);
+        if (a.h_err) (void)hipHostFree(a.h_err);
+    }
     if (p->stream) (void)hipStreamDestroy(p->stream);
     if (p->stream2) (void)hipStreamDestroy(p->stream2);
     if (p->copy_stream) (void)hipStreamDestroy(p->copy_stream);
@@ -525,6 +559,15 @@ msv_status msv_debug_set_stamps(msv_profile* p, uint64_t* d_stamps) {
     return MSV_OK;
 }
 
+// Diagnostics (not in msv.h): the host pipeline's piece plan -- the first piece is 1/first_den of the
+// batch, each next one `growth` times larger; first_den = 0 scores the batch as one piece.
+msv_status msv_debug_set_pipeline(msv_profile* p, uint32_t first_den, uint32_t growth) {
+    if (!p || growth == 0) return MSV_ERR_INVALID_ARGUMENT;
+    p->pipe_first_den = first_den;
+    p->pipe_growth = growth;
+    return MSV_OK;
+}
+
 int msv_debug_grid_waves(const msv_profile* p) {
     if (!p) return 0;
     const int lat = p->lat.v ? p->lat.blocks * p->lat.v->waves : 0;
@@ -564,9 +607,11 @@ msv_status msv_profile_describe(const msv_profile* p, msv_kernel_info* out) {
     return MSV_OK;
 }
 
-msv_status msv_score_batch_device(msv_profile* p, const uint8_t* d_residues, uint64_t residues_len,
-                                  const uint64_t* d_offsets, uint64_t n, const uint32_t* d_order, float* d_scores,
-                                  void* stream) {
+// One MSV launch.  `latency_ok`: a batch of few sequences may take the latency plan (not for the
+// pieces of a host pipeline, whose kernels must share the CUs with the next piece's).
+static msv_status launch_batch(msv_profile* p, const uint8_t* d_residues, uint64_t residues_len,
+                               const uint64_t* d_offsets, uint64_t n, const uint32_t* d_order, float* d_scores,
+                               void* stream, bool latency_ok, uint32_t* d_errors = nullptr) {
     if (!p) return MSV_ERR_INVALID_ARGUMENT;
     if (n == 0) return MSV_OK;
     if (!d_offsets || !d_scores || (residues_len && !d_residues)) return MSV_ERR_INVALID_ARGUMENT;
@@ -578,7 +623,7 @@ msv_status msv_score_batch_device(msv_profile* p, const uint8_t* d_residues, uin
     msvk::KernelArgs a{};
     // Small batches take the latency plan: with fewer sequences than ~4 per SIMD the launch lasts
     // one sequence's rows, and a 64-lane row is far shorter than a 16-lane one.
-    const Plan& plan = (p->lat.v && n <= p->lat_max_n) ? p->lat : p->main;
+    const Plan& plan = (latency_ok && p->lat.v && n <= p->lat_max_n) ? p->lat : p->main;
     a.etab = plan.d_etab;
     a.residues = residues_len ? d_residues : p->d_dummy;
     a.offsets = d_offsets;
@@ -600,13 +645,19 @@ msv_status msv_score_batch_device(msv_profile* p, const uint8_t* d_residues, uin
     int k = 0;
     MSV_HIP(p->kernels.acquire(st, &k));
     a.counter = p->d_words + 2 * k;
-    a.errors = p->d_words + kErrWord;
+    a.errors = d_errors ? d_errors : p->d_words + kErrWord;
     if (p->kernels.dirty[k]) MSV_HIP(hipMemsetAsync(a.counter, 0, 2 * sizeof(uint32_t), st));
     p->kernels.dirty[k] = true;
     MSV_HIP(msvk::launch_variant(*plan.v, dim3(blocks), a, st));
     p->kernels.dirty[k] = false;
     MSV_HIP(p->kernels.release(k, st));
     return MSV_OK;
+}
+
+msv_status msv_score_batch_device(msv_profile* p, const uint8_t* d_residues, uint64_t residues_len,
+                                  const uint64_t* d_offsets, uint64_t n, const uint32_t* d_order, float* d_scores,
+                                  void* stream) {
+    return launch_batch(p, d_residues, residues_len, d_offsets, n, d_order, d_scores, stream, true);
 }
 
 msv_status msv_profile_check(msv_profile* p, void* stream) {
@@ -667,7 +718,7 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     // previous piece's drain tail frees (each launch has its own dequeue counter slot).  Scores
     // come back in one D2H at the end (pageable destinations would make per-piece D2H copies
     // block the host thread that enqueues the pipeline).
-    const std::vector<uint64_t> cut = plan_pieces(offsets, n, total);
+    const std::vector<uint64_t> cut = plan_pieces(offsets, n, total, p->pipe_first_den, p->pipe_growth);
     const size_t P = cut.size() - 1;
     MSV_HIP(ensure(p->d_res, p->d_res_cap, std::max<uint64_t>(total, 1)));
     MSV_HIP(ensure(p->d_off, p->d_off_cap, n + P));
@@ -718,8 +769,8 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         // longest-first dequeue order of the piece (shorter drain tail; ~15-20% on 100k sequences)
         s = msv_order_longest_first(p, d_off, cn, p->d_order + cut[k], c);
         if (s != MSV_OK) return s;
-        s = msv_score_batch_device(p, bytes ? p->d_res + lo : p->d_dummy, std::max<uint64_t>(bytes, 1), d_off, cn,
-                                   p->d_order + cut[k], p->d_scores + cut[k], c);
+        s = launch_batch(p, bytes ? p->d_res + lo : p->d_dummy, std::max<uint64_t>(bytes, 1), d_off, cn,
+                         p->d_order + cut[k], p->d_scores + cut[k], c, !pipe);
         if (s != MSV_OK) return s;
     }
     if (pipe) {  // join the second compute stream back into the caller's
@@ -729,6 +780,84 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     MSV_HIP(hipMemcpyAsync(scores, p->d_scores, n * sizeof(float), hipMemcpyDeviceToHost, st));
     MSV_HIP(hipStreamSynchronize(st));  // pinned h_off is rewritten by the next call
     return msv_profile_check(p, st);
+}
+
+msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
+                                 float* scores, uint64_t* ticket) {
+    if (!p || !ticket || (n && (!offsets || !scores))) return MSV_ERR_INVALID_ARGUMENT;
+    *ticket = 0;
+    uint64_t maxL = 0;
+    for (uint64_t s = 0; s < n; ++s) {
+        if (offsets[s + 1] < offsets[s]) return MSV_ERR_INVALID_ARGUMENT;
+        maxL = std::max<uint64_t>(maxL, offsets[s + 1] - offsets[s]);
+    }
+    const uint64_t total = n ? offsets[n] - offsets[0] : 0;
+    if (total && !residues) return MSV_ERR_INVALID_ARGUMENT;
+    // one launch per call: split larger batches (or use msv_score_batch)
+    if (total >= kChunkBytes || n >= (1ull << 32) - (1ull << 24)) return MSV_ERR_INVALID_ARGUMENT;
+    auto& a = p->async[p->next_ticket % kAsyncSlots];
+    if (a.pending) return MSV_ERR_INVALID_ARGUMENT;  // that slot's call has not been waited for
+    msv_status s = msv_profile_reserve_length(p, maxL);
+    if (s != MSV_OK) return s;
+    DeviceGuard g(p->device);
+    if (!g.ok) return MSV_ERR_NO_DEVICE;
+    if (!p->copy_stream) MSV_HIP(hipStreamCreateWithFlags(&p->copy_stream, hipStreamNonBlocking));
+    if (!a.copied) MSV_HIP(hipEventCreateWithFlags(&a.copied, hipEventDisableTiming));
+    if (!a.done) MSV_HIP(hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
+    if (!a.h_err) MSV_HIP(hipHostMalloc(reinterpret_cast<void**>(&a.h_err), 64, hipHostMallocDefault));
+    MSV_HIP(ensure(a.d_res, a.res_cap, std::max<uint64_t>(total, 1)));
+    MSV_HIP(ensure(a.d_off, a.off_cap, n + 1));
+    MSV_HIP(ensure(a.d_sc, a.sc_cap, std::max<uint64_t>(n, 1)));
+    MSV_HIP(ensure(a.d_ord, a.ord_cap, std::max<uint64_t>(n, 1)));
+    if (a.h_cap < n + 1) {
+        if (a.h_off) (void)hipHostFree(a.h_off);
+        a.h_off = nullptr;
+        a.h_cap = 0;
+        MSV_HIP(hipHostMalloc(reinterpret_cast<void**>(&a.h_off), (n + 1) * sizeof(uint64_t), hipHostMallocDefault));
+        a.h_cap = n + 1;
+    }
+    const uint64_t base = n ? offsets[0] : 0;
+    for (uint64_t i = 0; i <= n; ++i) a.h_off[i] = n ? offsets[i] - base : 0;
+    const int slot = static_cast<int>(&a - p->async);
+    uint32_t* d_err = p->d_words + kErrWord + 1 + slot;
+    hipStream_t cp = p->copy_stream, cs = p->stream;
+    // copy stream: this call's inputs (they overlap the previous call's kernel on the compute stream)
+    MSV_HIP(hipMemcpyAsync(a.d_off, a.h_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, cp));
+    if (total) MSV_HIP(hipMemcpyAsync(a.d_res, residues + base, total, hipMemcpyHostToDevice, cp));
+    MSV_HIP(hipEventRecord(a.copied, cp));
+    // compute stream: order, kernel, scores and the slot's error word back to the host
+    MSV_HIP(hipStreamWaitEvent(cs, a.copied, 0));
+    if (n) {
+        s = msv_order_longest_first(p, a.d_off, n, a.d_ord, cs);
+        if (s != MSV_OK) return s;
+        s = launch_batch(p, total ? a.d_res : p->d_dummy, std::max<uint64_t>(total, 1), a.d_off, n, a.d_ord, a.d_sc,
+                         cs, true, d_err);
+        if (s != MSV_OK) return s;
+        MSV_HIP(hipMemcpyAsync(scores, a.d_sc, n * sizeof(float), hipMemcpyDeviceToHost, cs));
+    }
+    MSV_HIP(hipMemcpyAsync(a.h_err, d_err, sizeof(uint32_t), hipMemcpyDeviceToHost, cs));
+    MSV_HIP(hipMemsetAsync(d_err, 0, sizeof(uint32_t), cs));
+    MSV_HIP(hipEventRecord(a.done, cs));
+    a.ticket = p->next_ticket++;
+    a.pending = true;
+    *ticket = a.ticket;
+    return MSV_OK;
+}
+
+msv_status msv_profile_wait(msv_profile* p, uint64_t ticket) {
+    if (!p || ticket == 0) return MSV_ERR_INVALID_ARGUMENT;
+    for (auto& a : p->async) {
+        if (!a.pending || a.ticket != ticket) continue;
+        DeviceGuard g(p->device);
+        if (!g.ok) return MSV_ERR_NO_DEVICE;
+        MSV_HIP(hipEventSynchronize(a.done));
+        a.pending = false;
+        const uint32_t err = *a.h_err;
+        if (err & msvk::kErrBadResidue) return MSV_ERR_BAD_RESIDUE;
+        if (err & msvk::kErrTooLong) return MSV_ERR_SEQUENCE_TOO_LONG;
+        return MSV_OK;
+    }
+    return MSV_ERR_INVALID_ARGUMENT;  // unknown ticket, or already waited for
 }
 
 msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* d_residues,

@@ -174,6 +174,18 @@ msv_status msv_profile_reserve_length(msv_profile* profile, uint64_t max_length)
 msv_status msv_score_batch(msv_profile* profile, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
                            float* scores, void* stream);
 
+/* Asynchronous host-buffer scoring for a STREAM of batches (serving): enqueues the H2D of the
+ * inputs on the profile's copy stream and the order, kernel and score D2H on its compute stream, and
+ * returns at once with a ticket; msv_profile_wait(ticket) blocks until that call's scores are in
+ * `scores` and returns its kernel-latched errors.  Two staging sets, so the copy of call k+1 runs
+ * under the kernel of call k; at most 2 calls may be outstanding (a third returns
+ * MSV_ERR_INVALID_ARGUMENT until the oldest is waited for).  The caller keeps residues/offsets
+ * unchanged and does not read scores until the wait; pinned (page-locked) host buffers make the
+ * copies truly asynchronous.  One launch per call: residues < 2^32 - 2^20 bytes. */
+msv_status msv_score_batch_async(msv_profile* profile, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
+                                 float* scores, uint64_t* ticket);
+msv_status msv_profile_wait(msv_profile* profile, uint64_t ticket);
+
 /* Device-resident inputs and output (e.g. hipMalloc'd or torch tensors' data pointers), enqueued
  * on `stream` (a hipStream_t, NULL = the library's stream) without a host synchronisation.
  * residues_len = bytes addressable at d_residues (must be < 2^32 per call; split larger batches).

@@ -193,3 +193,37 @@ def test_describe_reports_both_plans():
     small = msv.MSV_HMM(msv.Profile_HMM(profile_path("100.hmm"))).describe()
     assert small["latency_variant"] == "" and small["latency_max_n"] == 0
     e.close()
+
+
+def test_async_stream_of_batches():
+    """msv_score_batch_async / msv_profile_wait: two calls in flight (copy of one under the kernel
+    of the other), results equal to the synchronous path; a bad residue is reported by the wait of
+    ITS call only; a third outstanding call is refused."""
+    import torch
+    from hmm_fasta_viterbi_amd._native import MSVError
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("1400.hmm")))
+    batches = [random_batch(400 + k, n, 0, 700) for k, n in enumerate((30_000, 1, 5_000, 60_000, 0, 12_345))]
+    want = [e.score_batch(codes=c, offsets=o) for c, o in batches]
+    pinned = [(torch.from_numpy(c).pin_memory().numpy(), o) for c, o in batches]
+    tickets = []
+    got = []
+    for k, (c, o) in enumerate(pinned):
+        tickets.append(e.score_batch_async(c, o))
+        if k >= 1:
+            got.append(e.wait(tickets[k - 1]))
+    got.append(e.wait(tickets[-1]))
+    for k, (g, w) in enumerate(zip(got, want)):
+        assert np.array_equal(bits(g), bits(w)), k
+    # errors stay with their call
+    bad_c = batches[0][0].copy()
+    bad_c[int(batches[0][1][9]) + 1] = 25
+    t_bad = e.score_batch_async(bad_c, batches[0][1])
+    t_ok = e.score_batch_async(batches[2][0], batches[2][1])
+    with pytest.raises(MSVError):
+        e.score_batch_async(batches[3][0], batches[3][1])  # two already outstanding
+    with pytest.raises(IndexError):
+        e.wait(t_bad)
+    assert np.array_equal(bits(e.wait(t_ok)), bits(want[2]))
+    with pytest.raises(MSVError):
+        e.wait(t_ok)  # already waited for
+    e.close()
