@@ -80,7 +80,17 @@ def host_cpus() -> dict:
 
 
 def cpu_threads(arg: int) -> int:
-    return arg if arg > 0 else max(1, host_cpus()["affinity_cpus"])
+    """One thread per CPU this process may run on, capped at the cgroup CPU quota when there is one
+    (on the GPU box the affinity mask is the whole 256-CPU host while the quota is 16 CPUs; 256
+    threads under that quota measured 4.31 M res/s against 4.97 for 16 on cfg3, so the cap is the
+    more generous baseline)."""
+    if arg > 0:
+        return arg
+    h = host_cpus()
+    n = h["affinity_cpus"]
+    if h["cgroup_cpu_quota"]:
+        n = min(n, max(1, int(-(-h["cgroup_cpu_quota"] // 1))))
+    return max(1, n)
 
 
 def cpu_model() -> str:
