@@ -151,7 +151,8 @@ struct LaunchRing {
     hipError_t acquire(hipStream_t st, int* slot) {
         const int k = static_cast<int>(next++ % kLaunchSlots);
         if (!done[k]) {
-            const hipError_t e = hipEventCreateWithFlags(&done[k], hipEventDisableTiming);
+            // device-scope release: the event only orders this device's streams
+            const hipError_t e = hipEventCreateWithFlags(&done[k], hipEventDisableTiming | hipEventReleaseToDevice);
             if (e != hipSuccess) return e;
         }
         if (last[k] && last[k] != st) {
@@ -203,7 +204,7 @@ struct msv_profile {
     std::vector<hipEvent_t> events;
     uint64_t* h_off = nullptr;
     size_t h_off_cap = 0;
-    uint32_t pipe_first_den = 16, pipe_growth = 2;  // piece sizes: total / first_den, then x growth
+    uint32_t pipe_first_den = 8, pipe_growth = 3;  // piece sizes: total / first_den, then x growth
     // msv_score_batch_async: kAsyncSlots staging sets, so the H2D of one call runs under the kernel
     // of the call before it
     struct AsyncSlot {
@@ -331,8 +332,8 @@ static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
 
 // Pieces of a host batch for msv_score_batch's copy/compute pipeline: cut[k] .. cut[k+1] is piece
 // k's sequence range.  Each piece addresses < kChunkBytes residues and < 2^32 - 2^24 sequences (one
-// launch each).  Batches below kPipelineMin residues are one piece; larger ones start at ~1/16 of the
-// batch (at least 1M residues) and double, a short remainder joining the last piece.
+// launch each).  Batches below kPipelineMin residues are one piece; larger ones start at 1/first_den
+// of the batch (at least 1M residues) and grow `growth`-fold, a short remainder joining the last piece.
 static std::vector<uint64_t> plan_pieces(const uint64_t* offsets, uint64_t n, uint64_t total, uint32_t first_den,
                                          uint32_t growth) {
     constexpr uint64_t kMaxSeqs = (1ull << 32) - (1ull << 24) - 1;
@@ -712,31 +713,29 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p->stream;
 
     // Copy/compute pipeline.  The batch is cut into pieces (contiguous sequence ranges) whose
-    // residue counts double from ~1/16 of the batch, so the first kernel starts after a short copy
-    // and every later piece's H2D (copy stream) runs under the kernels of the pieces before it.
-    // Pieces alternate between two compute streams, so a piece's kernel fills the CUs that the
-    // previous piece's drain tail frees (each launch has its own dequeue counter slot).  Scores
-    // come back in one D2H at the end (pageable destinations would make per-piece D2H copies
-    // block the host thread that enqueues the pipeline).
+    // residue counts grow geometrically from ~1/8 of the batch (x3: 3 pieces for cfg3, the best plan
+    // in tools/host_pipeline_sweep.py, profiles/r02_host_pipeline_sweep.jsonl), so the first kernel
+    // starts after a short copy and every later piece's H2D (copy stream) runs under the kernels of
+    // the pieces before it.  Piece k's offsets are rebased and sent right before its residues, and
+    // its longest-first order waits only for those offsets.  Pieces alternate between two compute
+    // streams, so a piece's kernel fills the CUs that the previous piece's drain tail frees (each
+    // launch has its own dequeue counter slot).  Scores and the error word come back once at the end
+    // (pageable destinations would make per-piece D2H copies block the host thread that enqueues the
+    // pipeline), followed by ONE synchronisation.
     const std::vector<uint64_t> cut = plan_pieces(offsets, n, total, p->pipe_first_den, p->pipe_growth);
     const size_t P = cut.size() - 1;
     MSV_HIP(ensure(p->d_res, p->d_res_cap, std::max<uint64_t>(total, 1)));
     MSV_HIP(ensure(p->d_off, p->d_off_cap, n + P));
     MSV_HIP(ensure(p->d_scores, p->d_scores_cap, n));
     MSV_HIP(ensure(p->d_order, p->d_order_cap, n));
-    if (p->h_off_cap < n + P) {  // pinned, so the offsets H2D is a true async DMA
+    if (p->h_off_cap < n + P + 8) {  // pinned, so the offsets H2D is a true async DMA (+ the error word)
         if (p->h_off) (void)hipHostFree(p->h_off);
         p->h_off = nullptr;
         p->h_off_cap = 0;
-        MSV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p->h_off), (n + P) * sizeof(uint64_t), hipHostMallocDefault));
-        p->h_off_cap = n + P;
+        MSV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p->h_off), (n + P + 8) * sizeof(uint64_t), hipHostMallocDefault));
+        p->h_off_cap = n + P + 8;
     }
-    // piece k's offsets, rebased on its first residue, at h_off[cut[k] + k .. cut[k+1] + k]
-    for (size_t k = 0; k < P; ++k) {
-        const uint64_t base = offsets[cut[k]];
-        uint64_t* o = p->h_off + cut[k] + k;
-        for (uint64_t i = cut[k]; i <= cut[k + 1]; ++i) o[i - cut[k]] = offsets[i] - base;
-    }
+    uint32_t* h_err = reinterpret_cast<uint32_t*>(p->h_off + n + P);
     const bool pipe = P > 1;
     hipStream_t cs[2] = {st, st}, cp = st;
     if (pipe) {
@@ -744,42 +743,52 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         if (!p->copy_stream) MSV_HIP(hipStreamCreateWithFlags(&p->copy_stream, hipStreamNonBlocking));
         cs[1] = p->stream2;
         cp = p->copy_stream;
-        while (p->events.size() < P + 2) {
+        while (p->events.size() < 2 * P + 2) {
             hipEvent_t e = nullptr;
-            MSV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            MSV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice));
             p->events.push_back(e);
         }
         // fork: both helper streams start after the caller's stream's earlier work
-        MSV_HIP(hipEventRecord(p->events[P], st));
-        MSV_HIP(hipStreamWaitEvent(cp, p->events[P], 0));
-        MSV_HIP(hipStreamWaitEvent(cs[1], p->events[P], 0));
+        MSV_HIP(hipEventRecord(p->events[2 * P], st));
+        MSV_HIP(hipStreamWaitEvent(cp, p->events[2 * P], 0));
+        MSV_HIP(hipStreamWaitEvent(cs[1], p->events[2 * P], 0));
     }
-    MSV_HIP(hipMemcpyAsync(p->d_off, p->h_off, (n + P) * sizeof(uint64_t), hipMemcpyHostToDevice, cp));
     const uint64_t base0 = offsets[0];
     for (size_t k = 0; k < P; ++k) {
         const uint64_t lo = offsets[cut[k]] - base0, bytes = offsets[cut[k + 1]] - offsets[cut[k]];
         const uint64_t cn = cut[k + 1] - cut[k];
-        if (bytes) MSV_HIP(hipMemcpyAsync(p->d_res + lo, residues + base0 + lo, bytes, hipMemcpyHostToDevice, cp));
+        // piece k's offsets, rebased on its first residue, at h_off[cut[k] + k .. cut[k+1] + k]
+        uint64_t* ho = p->h_off + cut[k] + k;
+        const uint64_t base = offsets[cut[k]];
+        for (uint64_t i = 0; i <= cn; ++i) ho[i] = offsets[cut[k] + i] - base;
+        uint64_t* d_off = p->d_off + cut[k] + k;
         hipStream_t c = cs[k & 1];
+        MSV_HIP(hipMemcpyAsync(d_off, ho, (cn + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, cp));
         if (pipe) {
-            MSV_HIP(hipEventRecord(p->events[k], cp));
-            MSV_HIP(hipStreamWaitEvent(c, p->events[k], 0));
+            MSV_HIP(hipEventRecord(p->events[2 * k], cp));
+            MSV_HIP(hipStreamWaitEvent(c, p->events[2 * k], 0));
         }
-        const uint64_t* d_off = p->d_off + cut[k] + k;
+        if (bytes) MSV_HIP(hipMemcpyAsync(p->d_res + lo, residues + base0 + lo, bytes, hipMemcpyHostToDevice, cp));
         // longest-first dequeue order of the piece (shorter drain tail; ~15-20% on 100k sequences)
         s = msv_order_longest_first(p, d_off, cn, p->d_order + cut[k], c);
         if (s != MSV_OK) return s;
+        if (pipe) {
+            MSV_HIP(hipEventRecord(p->events[2 * k + 1], cp));
+            MSV_HIP(hipStreamWaitEvent(c, p->events[2 * k + 1], 0));
+        }
         s = launch_batch(p, bytes ? p->d_res + lo : p->d_dummy, std::max<uint64_t>(bytes, 1), d_off, cn,
                          p->d_order + cut[k], p->d_scores + cut[k], c, !pipe);
         if (s != MSV_OK) return s;
     }
     if (pipe) {  // join the second compute stream back into the caller's
-        MSV_HIP(hipEventRecord(p->events[P + 1], cs[1]));
-        MSV_HIP(hipStreamWaitEvent(st, p->events[P + 1], 0));
+        MSV_HIP(hipEventRecord(p->events[2 * P + 1], cs[1]));
+        MSV_HIP(hipStreamWaitEvent(st, p->events[2 * P + 1], 0));
     }
     MSV_HIP(hipMemcpyAsync(scores, p->d_scores, n * sizeof(float), hipMemcpyDeviceToHost, st));
-    MSV_HIP(hipStreamSynchronize(st));  // pinned h_off is rewritten by the next call
-    return msv_profile_check(p, st);
+    MSV_HIP(hipMemcpyAsync(h_err, p->d_words + kErrWord, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    MSV_HIP(hipStreamSynchronize(st));  // also: the pinned h_off is rewritten by the next call
+    if (*h_err == 0) return MSV_OK;
+    return msv_profile_check(p, st);  // reads, clears and reports the latched error bits
 }
 
 msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const uint64_t* offsets, uint64_t n,

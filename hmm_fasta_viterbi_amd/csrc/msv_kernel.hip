@@ -170,7 +170,7 @@ template <int PF>
 struct RowCtx {
     static constexpr int kPF = PF;
     const float4* ep;
-    float Bt, nbr, p0, p1;
+    float Bt, nbr, p0, p1, p2, p3;  // (p2, p3 unused: keeping them keeps the register assignment measured in round 1)
     uint8_t rnext;   // residue code RPF rows ahead
     float4 ring[PF];
 };

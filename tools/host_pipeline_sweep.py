@@ -36,7 +36,7 @@ def main():
     pinned = torch.from_numpy(codes).pin_memory().numpy()
     L = _native.lib()
     L.msv_debug_set_pipeline.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
-    plans = [(0, 2), (16, 2), (8, 2), (4, 2), (8, 3), (12, 2), (6, 2), (32, 2), (4, 3)]
+    plans = [(0, 2), (8, 3), (6, 2), (12, 3), (10, 2), (16, 4), (5, 3)]
     res = int(offsets[-1])
     want = e.score_batch(codes=codes, offsets=offsets)
     for _ in range(10):  # clock ramp

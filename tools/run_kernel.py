@@ -1,6 +1,9 @@
 """Run the MSV kernel alone on a BASELINE config (for rocprofv3 --kernel-trace / --pmc passes).
 
-    python tools/run_kernel.py --config cfg3 --launches 5 [--variant NAME] [--no-order]
+    python tools/run_kernel.py --config cfg3 --launches 5 [--variant NAME] [--no-order] [--time K]
+
+--time K: after the launches (warm-up), time K more with HIP events on the launch stream and print
+one JSON line (kernel ms; A/B of library builds via MSV_LIB_PATH, tools/kernel_ab.py).
 """
 import argparse
 import os
@@ -18,13 +21,14 @@ def main():
     ap.add_argument("--launches", type=int, default=5)
     ap.add_argument("--variant", default="")
     ap.add_argument("--no-order", action="store_true")
+    ap.add_argument("--time", type=int, default=0)
     args = ap.parse_args()
     import torch
     import hmm_fasta_viterbi_amd as msv
     from hmm_fasta_viterbi_amd.synthetic import random_batch
     from bench import CONFIGS
 
-    prof, n, lmin, lmax, seed = CONFIGS[args.config]
+    prof, n, lmin, lmax, seed = CONFIGS[args.config][:5]
     eng = msv.MSV_HMM(msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof)))
     if args.variant:
         eng.set_variant(args.variant)
@@ -42,6 +46,19 @@ def main():
     for _ in range(args.launches):
         eng.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), n, s.data_ptr(), op, st.cuda_stream)
     eng.check(st.cuda_stream)
+    if args.time:
+        import json
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.time)]
+        for a, b in ev:
+            a.record(st)
+            eng.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), n, s.data_ptr(), op, st.cuda_stream)
+            b.record(st)
+        eng.check(st.cuda_stream)
+        ms = sorted(a.elapsed_time(b) for a, b in ev)
+        print(json.dumps({"config": args.config, "lib": os.environ.get("MSV_LIB_PATH", "in-tree"),
+                          "variant": eng.describe()["variant"], "kernel_ms_mean": sum(ms) / len(ms),
+                          "kernel_ms_median": ms[len(ms) // 2], "kernel_ms_min": ms[0]}), flush=True)
+        return
     print(f"{args.config}: {eng.describe()['variant']} x {args.launches} launches, residues={int(offsets[-1])}, "
           f"LENG={eng.model_length - 1}")
 
