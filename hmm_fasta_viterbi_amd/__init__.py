@@ -224,6 +224,11 @@ class MSV_HMM:
     def order_longest_first(self, offsets_ptr: int, n: int, order_ptr: int, stream: int | None = None) -> None:
         check(_native.lib().msv_order_longest_first(self._p, offsets_ptr, n, order_ptr, stream))
 
+    def bind_stream(self, stream: int | None) -> None:
+        """Declare `stream` (a hipStream_t handle that outlives the binding) as this profile's working
+        stream: its launches skip the per-launch slot event (msv_profile_bind_stream).  None unbinds."""
+        check(_native.lib().msv_profile_bind_stream(self._p, stream), "msv_profile_bind_stream")
+
     def check(self, stream: int | None = None) -> None:
         st = _native.lib().msv_profile_check(self._p, stream)
         if st == _native.MSV_ERR_BAD_RESIDUE:

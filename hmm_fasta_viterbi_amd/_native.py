@@ -45,7 +45,7 @@ EXPORTED = [
     "msv_fasta_device_rejected", "msv_fasta_device_residues", "msv_fasta_device_codes", "msv_fasta_device_offsets",
     "msv_fasta_device_header_spans", "msv_fasta_device_text", "msv_fasta_device_download",
     "msv_fasta_device_max_length", "msv_score_fasta_device", "msv_fasta_device_device",
-    "msv_score_batch_async", "msv_profile_wait",
+    "msv_score_batch_async", "msv_profile_wait", "msv_profile_bind_stream",
 ]
 
 
@@ -132,6 +132,7 @@ def lib() -> C.CDLL:
         "msv_score_batch_device": (C.c_int, [vp, vp, u64, vp, u64, vp, vp, vp]),
         "msv_score_batch_async": (C.c_int, [vp, vp, vp, u64, vp, C.POINTER(C.c_uint64)]),
         "msv_profile_wait": (C.c_int, [vp, u64]),
+        "msv_profile_bind_stream": (C.c_int, [vp, vp]),
         "msv_profile_check": (C.c_int, [vp, vp]),
         "msv_order_longest_first": (C.c_int, [vp, vp, u64, vp, vp]),
         "msv_variant_count": (C.c_int, []),

@@ -139,10 +139,15 @@ const msvk::Variant* pick_variant(uint32_t states) {
 }
 
 // Launch slots of one profile (see kLaunchSlots): the stream and completion event of each slot's
-// last launch.
+// last launch.  An event record is a packet on the stream (~4 us between a launch and the next
+// one, 3% of a 0.14 ms cfg2 kernel), so it is recorded lazily -- only when another stream wants
+// the slot -- for streams known to outlive that moment: the library's own streams and the stream
+// the caller bound with msv_profile_bind_stream.  A launch on any other caller stream records its
+// event at once (that stream may be destroyed before the next launch).
 struct LaunchRing {
     hipEvent_t done[kLaunchSlots] = {};
     hipStream_t last[kLaunchSlots] = {};  // nullptr: never launched
+    bool recorded[kLaunchSlots] = {};     // done[k] covers the slot's last launch
     bool dirty[kLaunchSlots] = {};        // a launch failed after the slot's counters were touched
     uint32_t next = 0;
 
@@ -156,15 +161,32 @@ struct LaunchRing {
             if (e != hipSuccess) return e;
         }
         if (last[k] && last[k] != st) {
+            if (!recorded[k]) {  // lazy: last[k] is a live stream; this covers all of its work so far
+                const hipError_t e = hipEventRecord(done[k], last[k]);
+                if (e != hipSuccess) return e;
+                recorded[k] = true;
+            }
             const hipError_t e = hipStreamWaitEvent(st, done[k], 0);
             if (e != hipSuccess) return e;
         }
         *slot = k;
         return hipSuccess;
     }
-    hipError_t release(int k, hipStream_t st) {
+    // `lazy`: `st` is known to stay alive until the next acquire of this slot or flush()
+    hipError_t release(int k, hipStream_t st, bool lazy) {
         last[k] = st;
-        return hipEventRecord(done[k], st);
+        recorded[k] = !lazy;
+        return lazy ? hipSuccess : hipEventRecord(done[k], st);
+    }
+    // Records the pending lazy events of stream `st` (before it stops being guaranteed alive).
+    hipError_t flush(hipStream_t st) {
+        for (int k = 0; k < kLaunchSlots; ++k)
+            if (last[k] == st && !recorded[k]) {
+                const hipError_t e = hipEventRecord(done[k], st);
+                if (e != hipSuccess) return e;
+                recorded[k] = true;
+            }
+        return hipSuccess;
     }
     void destroy() {
         for (hipEvent_t& e : done)
@@ -198,6 +220,7 @@ struct msv_profile {
     uint8_t* d_dummy = nullptr;   // a readable residue byte for batches with no residues
     LaunchRing kernels, orders;   // launch slots of the MSV kernel and of the order sort
     hipStream_t stream = nullptr;
+    hipStream_t bound = nullptr;  // msv_profile_bind_stream: a caller stream guaranteed alive while bound
     // host-API pipeline (msv_score_batch): a second compute stream, a copy stream, piece events,
     // and pinned staging for the rebased offsets
     hipStream_t stream2 = nullptr, copy_stream = nullptr;
@@ -237,6 +260,12 @@ struct msv_profile {
     hipEvent_t done = nullptr;     // grid API: joins this profile's stream back to the caller's
 };
 
+
+// Streams on which a launch may leave its slot event unrecorded (LaunchRing): they stay alive
+// until the profile is destroyed or the binding ends (msv_profile_bind_stream flushes first).
+static bool lazy_stream(const msv_profile* p, hipStream_t st) {
+    return st == p->stream || st == p->stream2 || (p->bound && st == p->bound);
+}
 
 // Lays the MSV table out for variant v and uploads it:
 // [row r][chunk c][lane gl] float4 = e[r][gl*S + 4c + 1 .. +4]; states beyond LENG are -inf
@@ -651,7 +680,7 @@ static msv_status launch_batch(msv_profile* p, const uint8_t* d_residues, uint64
     p->kernels.dirty[k] = true;
     MSV_HIP(msvk::launch_variant(*plan.v, dim3(blocks), a, st));
     p->kernels.dirty[k] = false;
-    MSV_HIP(p->kernels.release(k, st));
+    MSV_HIP(p->kernels.release(k, st, lazy_stream(p, st)));
     return MSV_OK;
 }
 
@@ -659,6 +688,20 @@ msv_status msv_score_batch_device(msv_profile* p, const uint8_t* d_residues, uin
                                   const uint64_t* d_offsets, uint64_t n, const uint32_t* d_order, float* d_scores,
                                   void* stream) {
     return launch_batch(p, d_residues, residues_len, d_offsets, n, d_order, d_scores, stream, true);
+}
+
+msv_status msv_profile_bind_stream(msv_profile* p, void* stream) {
+    if (!p) return MSV_ERR_INVALID_ARGUMENT;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (st == p->bound) return MSV_OK;
+    DeviceGuard g(p->device);
+    if (!g.ok) return MSV_ERR_NO_DEVICE;
+    if (p->bound) {  // the old stream loses its guarantee: record what is still pending on it
+        MSV_HIP(p->kernels.flush(p->bound));
+        MSV_HIP(p->orders.flush(p->bound));
+    }
+    p->bound = st;
+    return MSV_OK;
 }
 
 msv_status msv_profile_check(msv_profile* p, void* stream) {
@@ -688,7 +731,7 @@ msv_status msv_order_longest_first(msv_profile* p, const uint64_t* d_offsets, ui
     int k = 0;
     MSV_HIP(p->orders.acquire(st, &k));
     MSV_HIP(msvk::launch_order(d_offsets, n, p->d_hist + static_cast<size_t>(k) * kOrderBins, kOrderBins, d_order, st));
-    MSV_HIP(p->orders.release(k, st));
+    MSV_HIP(p->orders.release(k, st, lazy_stream(p, st)));
     return MSV_OK;
 }
 

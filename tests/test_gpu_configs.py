@@ -168,6 +168,9 @@ def test_one_profile_on_two_streams_without_sync():
         assert np.array_equal(bits(host), bits(ref[1])), rep
         for k in (0, 2, 3):
             assert np.array_equal(bits(tens[k][2].cpu().numpy()), bits(ref[k])), (rep, k)
+        # rep 1: stream 0 bound (its slot events are recorded lazily, only when another stream takes
+        # the slot); rep 2: unbound again (the pending events are flushed first)
+        e.bind_stream(streams[0].cuda_stream if rep == 0 else None)
     e.close()
 
 
