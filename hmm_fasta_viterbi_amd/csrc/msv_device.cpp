@@ -228,6 +228,7 @@ struct msv_profile {
     uint64_t* h_off = nullptr;
     size_t h_off_cap = 0;
     uint32_t pipe_first_den = 8, pipe_growth = 3;  // piece sizes: total / first_den, then x growth
+    uint32_t pipe_streams = 2;                      // compute streams the pieces alternate over
     // msv_score_batch_async: kAsyncSlots staging sets, so the H2D of one call runs under the kernel
     // of the call before it
     struct AsyncSlot {
@@ -590,11 +591,13 @@ msv_status msv_debug_set_stamps(msv_profile* p, uint64_t* d_stamps) {
 }
 
 // Diagnostics (not in msv.h): the host pipeline's piece plan -- the first piece is 1/first_den of the
-// batch, each next one `growth` times larger; first_den = 0 scores the batch as one piece.
-msv_status msv_debug_set_pipeline(msv_profile* p, uint32_t first_den, uint32_t growth) {
-    if (!p || growth == 0) return MSV_ERR_INVALID_ARGUMENT;
+// batch, each next one `growth` times larger; first_den = 0 scores the batch as one piece; pieces
+// alternate over `streams` (1 or 2) compute streams.
+msv_status msv_debug_set_pipeline(msv_profile* p, uint32_t first_den, uint32_t growth, uint32_t streams) {
+    if (!p || growth == 0 || streams < 1 || streams > 2) return MSV_ERR_INVALID_ARGUMENT;
     p->pipe_first_den = first_den;
     p->pipe_growth = growth;
+    p->pipe_streams = streams;
     return MSV_OK;
 }
 
@@ -784,7 +787,7 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     if (pipe) {
         if (!p->stream2) MSV_HIP(hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking));
         if (!p->copy_stream) MSV_HIP(hipStreamCreateWithFlags(&p->copy_stream, hipStreamNonBlocking));
-        cs[1] = p->stream2;
+        cs[1] = p->pipe_streams == 2 ? p->stream2 : st;
         cp = p->copy_stream;
         while (p->events.size() < 2 * P + 2) {
             hipEvent_t e = nullptr;

@@ -35,15 +35,15 @@ def main():
     codes, offsets = random_batch(seed * 1000, n, lmin, lmax)
     pinned = torch.from_numpy(codes).pin_memory().numpy()
     L = _native.lib()
-    L.msv_debug_set_pipeline.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
-    plans = [(0, 2), (8, 3), (6, 2), (12, 3), (10, 2), (16, 4), (5, 3)]
+    L.msv_debug_set_pipeline.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32]
+    plans = [(0, 2, 1), (8, 3, 2), (8, 3, 1), (6, 2, 2), (6, 2, 1), (5, 2, 2), (7, 2, 2)]
     res = int(offsets[-1])
     want = e.score_batch(codes=codes, offsets=offsets)
     for _ in range(10):  # clock ramp
         e.score_batch(codes=pinned, offsets=offsets)
     for r in range(a.rounds):
-        for den, g in plans:
-            assert L.msv_debug_set_pipeline(e._p, den, g) == 0
+        for den, g, ns in plans:
+            assert L.msv_debug_set_pipeline(e._p, den, g, ns) == 0
             for _ in range(2):
                 e.score_batch(codes=pinned, offsets=offsets)
             t = time.perf_counter()
@@ -51,7 +51,7 @@ def main():
                 out = e.score_batch(codes=pinned, offsets=offsets)
             ms = (time.perf_counter() - t) / a.calls * 1e3
             ok = bool(np.array_equal(out.view(np.uint32), want.view(np.uint32)))
-            print(json.dumps({"config": a.config, "round": r, "first_den": den, "growth": g, "ms": round(ms, 4),
+            print(json.dumps({"config": a.config, "round": r, "first_den": den, "growth": g, "streams": ns, "ms": round(ms, 4),
                               "M_residues_s": round(res / ms / 1e3, 1), "bitwise_equal": ok}), flush=True)
 
 
