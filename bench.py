@@ -38,8 +38,10 @@ sys.path.insert(0, ROOT)
 # The host pipeline (msv_score_batch / msv_score_batch_async) keeps a copy stream and two compute
 # streams busy at once next to torch's streams; HIP's default of 4 hardware queues per process then
 # makes streams share queues and serialise (cfg3 pipelined host path 9,543 vs 10,597 M res/s with 8).
-# Informational figures only; the HBM-resident `value` runs on one stream.  (Before torch loads HIP.)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# Informational figures only; the HBM-resident `value` runs on one stream.  (Set before torch loads
+# HIP; the GPU box exports 4.)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 CONFIGS = {
     # name: (profile, sequences, lmin, lmax, seed, scaling)  -- SURVEY 8(d) / BASELINE.md

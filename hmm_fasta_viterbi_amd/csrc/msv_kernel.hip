@@ -198,6 +198,14 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // chunks are requested right after this row's last cell update, so the LDS latency hides behind
     // the E butterfly and the specials instead of stalling the start of every row.
     constexpr bool XROW = !BIG && !SPLIT && D == 1 && PF >= C4 && St::RPF >= 2;
+    // ... and two rows ahead when the residue slots rotate over an even number of phases: rows of
+    // even and odd phase keep their own ring, refilled with the row after next right after use, so
+    // the LDS reads have a whole row to land instead of the epilogue's dozen instructions (cfg2:
+    // 100.hmm rows are ~35 VALU, and waves spent 67% of their cycles in s_waitcnt, PMC r02).
+#ifndef MSV_XROW_DEPTH
+#define MSV_XROW_DEPTH 2
+#endif
+    constexpr bool XROW2 = XROW && MSV_XROW_DEPTH == 2 && St::RPF % 2 == 0 && PF <= 2;  // +4 PF VGPRs
     static_assert(SPLIT || BIG == (LDS_ROWS < kTableRows), "BIG <=> table does not fit LDS");
     __shared__ float4 tab[LDS_ROWS * ROW_F4];
 
@@ -505,8 +513,9 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // (Branch-layout hints -- __builtin_expect on the rare end-of-sequence / prefetch events, or on
     // the LDS-row class for G = 64 -- measured no gain, and 15% LOSS for the latter on 2405.hmm.)
 
-    RowCtx<PF> xr;  // XROW: the ring persists across rows
+    RowCtx<PF> xr, xr1;  // XROW: the ring persists across rows (XROW2: xr for even phases, xr1 for odd)
     if constexpr (XROW) fill_ring(xr, row_ptr(s0, Ph0{}));
+    if constexpr (XROW2) fill_ring(xr1, lds_row(s0.r[1]));
     fill_b(s0.r[0]);
 
     // slot of the residue of the row after a row of phase P
@@ -536,9 +545,19 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // One row of phase P of the single-stream, non-row-class paths (XROW or plain), then its events.
     // Returns whether the wave still has work.
     auto step = [&](auto ph) -> bool {
-        constexpr int PN = (decltype(ph)::value + 1) % St::RPF;
+        constexpr int PH = decltype(ph)::value;
+        constexpr int PN = (PH + 1) % St::RPF;
         using PhN = std::integral_constant<int, PN>;
-        if constexpr (XROW) {
+        if constexpr (XROW2) {
+            RowCtx<PF>& rc = (PH & 1) ? xr1 : xr;
+            prologue(s0, rc, nullptr, ph);
+            [&]<int... I>(std::integer_sequence<int, I...>) {
+                ((chunk(s0, rc, std::integral_constant<int, C4 - 1 - I>{})), ...);
+            }(std::make_integer_sequence<int, C4>{});
+            // r[PH + 2] is the residue of the row after next (discarded if the sequence ends first)
+            fill_ring(rc, lds_row(s0.r[(PH + 2) % St::RPF]));
+            epilogue(s0, rc, ph);
+        } else if constexpr (XROW) {
             prologue(s0, xr, nullptr, ph);
             [&]<int... I>(std::integer_sequence<int, I...>) {
                 ((chunk(s0, xr, std::integral_constant<int, C4 - 1 - I>{})), ...);
@@ -558,7 +577,12 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             }
             if (s0.pos == s0.endp) {
                 finish(s0, PhN{});
-                if constexpr (XROW) fill_ring(xr, row_ptr(s0, PhN{}));
+                if constexpr (XROW2) {  // the new sequence's first two rows
+                    fill_ring((PN & 1) ? xr1 : xr, row_ptr(s0, PhN{}));
+                    fill_ring((PN & 1) ? xr : xr1, lds_row(s0.r[(PN + 1) % St::RPF]));
+                } else if constexpr (XROW) {
+                    fill_ring(xr, row_ptr(s0, PhN{}));
+                }
                 fill_b(s0.r[PN]);
             }
             live = __any(s0.active);
