@@ -25,7 +25,7 @@ from ._native import MSVError, check
 __all__ = [
     "AMINO_ACIDS", "MSVError", "Profile_HMM", "FASTA_protein_sequences", "MSV_HMM", "pack_sequences",
     "encode", "sequence_transitions", "device_count", "score_grid", "score_grid_device", "score_batch_multi",
-    "shard_bounds", "FASTA_device",
+    "shard_bounds", "FASTA_device", "MultiGPU",
 ]
 
 AMINO_ACIDS = "ACDEFGHIKLMNPQRSTVWY"  # MSV_HMM.cpp:29-31
@@ -361,6 +361,45 @@ def score_batch_multi(engines: Sequence[MSV_HMM], seqs: Sequence[str] | None = N
         raise IndexError("residue outside the 20 amino acids")
     check(st, "msv_score_batch_multi")
     return out
+
+
+class MultiGPU:
+    """One batch over several GPUs from this process, scores gathered over RCCL (msv_multi_*):
+    engines[k] = the same model on DISTINCT devices; residue-balanced shards, one grouped RCCL
+    send/recv into device 0, one D2H."""
+
+    def __init__(self, engines: Sequence[MSV_HMM]):
+        if not engines:
+            raise ValueError("MultiGPU needs at least one engine")
+        self._engines = list(engines)  # the context refers to their profiles
+        m = C.c_void_p()
+        check(_native.lib().msv_multi_create(_handles(self._engines), len(self._engines), C.byref(m)),
+              "msv_multi_create")
+        self._m = m
+
+    def score_batch(self, seqs: Sequence[str] | None = None, *, codes: np.ndarray | None = None,
+                    offsets: np.ndarray | None = None) -> np.ndarray:
+        if seqs is not None:
+            codes, offsets = pack_sequences(seqs)
+        codes = np.ascontiguousarray(codes, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        n = len(offsets) - 1
+        out = np.zeros(n, np.float32)
+        st = _native.lib().msv_multi_score_batch(self._m, codes.ctypes.data if codes.size else None,
+                                                 offsets.ctypes.data, n, out.ctypes.data)
+        if st == _native.MSV_ERR_BAD_RESIDUE:
+            raise IndexError("residue outside the 20 amino acids")
+        check(st, "msv_multi_score_batch")
+        return out
+
+    def close(self):
+        lib = _loaded_lib()
+        if getattr(self, "_m", None) and lib is not None:
+            lib.msv_multi_destroy(self._m)
+            self._m = None
+
+    def __del__(self):
+        self.close()
 
 
 class FASTA_device:

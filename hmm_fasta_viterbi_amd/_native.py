@@ -24,6 +24,7 @@ STATUS = {
     7: "MSV_ERR_NO_DEVICE",
     8: "MSV_ERR_HIP",
     9: "MSV_ERR_OUT_OF_MEMORY",
+    10: "MSV_ERR_RCCL",
 }
 MSV_OK = 0
 MSV_ERR_BAD_RESIDUE = 4
@@ -46,6 +47,7 @@ EXPORTED = [
     "msv_fasta_device_header_spans", "msv_fasta_device_text", "msv_fasta_device_download",
     "msv_fasta_device_max_length", "msv_score_fasta_device", "msv_fasta_device_device",
     "msv_score_batch_async", "msv_profile_wait", "msv_profile_bind_stream",
+    "msv_multi_create", "msv_multi_score_batch", "msv_multi_destroy",
 ]
 
 
@@ -133,6 +135,9 @@ def lib() -> C.CDLL:
         "msv_score_batch_async": (C.c_int, [vp, vp, vp, u64, vp, C.POINTER(C.c_uint64)]),
         "msv_profile_wait": (C.c_int, [vp, u64]),
         "msv_profile_bind_stream": (C.c_int, [vp, vp]),
+        "msv_multi_create": (C.c_int, [vp, C.c_uint32, C.POINTER(vp)]),
+        "msv_multi_score_batch": (C.c_int, [vp, vp, vp, u64, vp]),
+        "msv_multi_destroy": (None, [vp]),
         "msv_profile_check": (C.c_int, [vp, vp]),
         "msv_order_longest_first": (C.c_int, [vp, vp, u64, vp, vp]),
         "msv_variant_count": (C.c_int, []),

@@ -403,6 +403,7 @@ const char* msv_status_string(msv_status s) {
         case MSV_ERR_NO_DEVICE: return "MSV_ERR_NO_DEVICE";
         case MSV_ERR_HIP: return "MSV_ERR_HIP";
         case MSV_ERR_OUT_OF_MEMORY: return "MSV_ERR_OUT_OF_MEMORY";
+        case MSV_ERR_RCCL: return "MSV_ERR_RCCL";
     }
     return "MSV_ERR_UNKNOWN";
 }

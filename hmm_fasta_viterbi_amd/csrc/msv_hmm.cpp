@@ -170,3 +170,24 @@ std::vector<Log_score> MSV_HMM::score_batch(const uint8_t* codes, const uint64_t
     check(s, "msv_score_batch");
     return out;
 }
+
+MSV_HMM::Multi_device::Multi_device(const std::vector<MSV_HMM*>& per_device) {
+    std::vector<msv_profile*> handles;
+    for (MSV_HMM* m : per_device) handles.push_back(m->profile_);
+    check(msv_multi_create(handles.data(), static_cast<uint32_t>(handles.size()), &multi_), "msv_multi_create");
+}
+
+MSV_HMM::Multi_device::~Multi_device() { msv_multi_destroy(multi_); }
+
+std::vector<Log_score> MSV_HMM::Multi_device::score_batch(const Protein_sequences& seqs) {
+    return score_batch(Packed_sequences::pack(seqs));
+}
+
+std::vector<Log_score> MSV_HMM::Multi_device::score_batch(const Packed_sequences& packed) {
+    std::vector<Log_score> out(packed.size());
+    const msv_status s =
+        msv_multi_score_batch(multi_, packed.codes.data(), packed.offsets.data(), packed.size(), out.data());
+    if (s == MSV_ERR_BAD_RESIDUE) throw std::out_of_range("residue outside the 20 amino acids");
+    check(s, "msv_multi_score_batch");
+    return out;
+}

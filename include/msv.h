@@ -39,7 +39,8 @@ typedef enum msv_status {
     MSV_ERR_UNSUPPORTED_MODEL = 6,/* model length outside the compiled kernel family          */
     MSV_ERR_NO_DEVICE = 7,        /* no HIP device / bad device ordinal                        */
     MSV_ERR_HIP = 8,              /* a HIP runtime call failed                                 */
-    MSV_ERR_OUT_OF_MEMORY = 9
+    MSV_ERR_OUT_OF_MEMORY = 9,
+    MSV_ERR_RCCL = 10             /* an RCCL call failed (multi-GPU context)                   */
 } msv_status;
 
 typedef struct msv_hmm msv_hmm;         /* parsed HMMER3 profile (host)            */
@@ -246,6 +247,22 @@ msv_status msv_shard_bounds(const uint64_t* offsets, uint64_t n, uint32_t n_shar
  * then scores its shards one after another on one thread. */
 msv_status msv_score_batch_multi(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* residues,
                                  const uint64_t* offsets, uint64_t n, float* scores);
+
+/* ---- several devices from one process, scores gathered over RCCL --------------
+ * A context over profiles[k] = the same model created on DISTINCT devices (rank k = profiles[k]'s
+ * device; one RCCL communicator per device from ncclCommInitAll).  msv_multi_score_batch cuts the
+ * batch into residue-balanced contiguous shards (msv_shard_bounds), one host thread per device uploads
+ * its shard and enqueues the longest-first order and the kernel on the context's stream for that
+ * device, then ONE RCCL group (ncclSend from every rank, ncclRecv into device 0's buffer at the
+ * shard's offset -- exact counts, rank 0 included through a self send/recv) gathers the float scores
+ * on device 0, and a single D2H returns them in input order.  A device listed twice is
+ * MSV_ERR_INVALID_ARGUMENT (one rank per device); RCCL failures are MSV_ERR_RCCL.  The context
+ * holds the profiles by pointer: destroy it before them. */
+typedef struct msv_multi msv_multi;
+msv_status msv_multi_create(msv_profile* const* profiles, uint32_t n_profiles, msv_multi** out);
+msv_status msv_multi_score_batch(msv_multi* multi, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
+                                 float* scores);
+void msv_multi_destroy(msv_multi* multi);
 
 /* ---- MSV filter P-values -----------------------------------------------------
  * The reference parses STATS LOCAL MSV mu/lambda (data_readers/Profile_HMM.cpp:73-94) and never

@@ -121,6 +121,9 @@ class MSV_HMM {
     static std::vector<Log_score> score_batch_multi(const std::vector<MSV_HMM*>& per_device,
                                                     const Protein_sequences& seqs);
 
+    // One batch over several devices of this process, scores gathered over RCCL (msv_multi_*).
+    class Multi_device;
+
     msv_profile* handle() { return profile_; }
     size_t model_length() const { return model_length_; }
     const std::vector<float>& emission_scores() const { return emission_scores_; }
@@ -133,4 +136,20 @@ class MSV_HMM {
     std::vector<float> emission_scores_;  // [20][model_length], MSV_HMM.hpp:27-28
     float tr_B_Mk_ = 0, tr_E_C_ = 0, tr_E_J_ = 0;
     msv_profile* profile_ = nullptr;
+};
+
+// MSV_HMM::Multi_device: the same model on DISTINCT devices (per_device[k] on device k), one RCCL
+// communicator per device; score_batch shards the batch by residues and gathers the scores on the
+// first device over RCCL (msv_multi_create / msv_multi_score_batch).  Holds the MSV_HMMs by pointer.
+class MSV_HMM::Multi_device {
+  public:
+    explicit Multi_device(const std::vector<MSV_HMM*>& per_device);
+    ~Multi_device();
+    Multi_device(const Multi_device&) = delete;
+    Multi_device& operator=(const Multi_device&) = delete;
+    std::vector<Log_score> score_batch(const Protein_sequences& seqs);
+    std::vector<Log_score> score_batch(const Packed_sequences& packed);
+
+  private:
+    msv_multi* multi_ = nullptr;
 };

@@ -125,6 +125,20 @@ int main(int argc, char** argv) {
             }
         }
     }
+    // one device through the RCCL multi-device context (1-rank communicator; the shard's scores take
+    // the self send/recv path of the gather) equals one launch
+    {
+        auto m = MSV_HMM(Profile_HMM(root + "/data/profile_HMMs/1400.hmm"));
+        MSV_HMM::Multi_device multi({&m});
+        auto got = multi.score_batch(fasta.sequences);
+        auto want = m.score_batch(fasta.sequences);
+        for (size_t i = 0; i < want.size(); ++i)
+            if (!same_bits(got[i], want[i])) {
+                std::printf("test_msv failed! RCCL multi-device seq %zu: %a vs %a\n", i, got[i], want[i]);
+                return 1;
+            }
+        checked += static_cast<int>(want.size());
+    }
     // error behaviour: a residue outside the 20 throws std::out_of_range like amino_acid_num.at
     auto msv = MSV_HMM(Profile_HMM(root + "/data/profile_HMMs/100.hmm"));
     bool threw = false;

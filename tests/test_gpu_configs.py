@@ -230,3 +230,30 @@ def test_async_stream_of_batches():
     with pytest.raises(MSVError):
         e.wait(t_ok)  # already waited for
     e.close()
+
+
+def test_rccl_multi_device_context():
+    """msv_multi_*: ncclCommInitAll over the given devices, shards scored per device, scores gathered
+    into device 0 by ONE grouped ncclSend/ncclRecv (rank 0 through a self send/recv), one D2H.  On a
+    one-GPU box this is a 1-rank communicator (the exchange still runs, as a self send/recv); with
+    more devices every visible one joins.  A device listed twice is refused (one RCCL rank per
+    device: RCCL rejects duplicate GPUs in one communicator)."""
+    from hmm_fasta_viterbi_amd._native import MSVError
+    prof = msv.Profile_HMM(profile_path("1400.hmm"))
+    ndev = msv.device_count()
+    engines = [msv.MSV_HMM(prof, device=k) for k in range(ndev)]
+    codes, offsets = random_batch(3, 200_000, 300, 500)  # cfg4's generator, 200k of its 1M
+    want = engines[0].score_batch(codes=codes, offsets=offsets)
+    multi = msv.MultiGPU(engines)
+    got = multi.score_batch(codes=codes, offsets=offsets)
+    assert np.array_equal(bits(got), bits(want))
+    small = multi.score_batch(codes=codes[:int(offsets[3])], offsets=offsets[:4])  # fewer sequences than ranks
+    assert np.array_equal(bits(small), bits(want[:3]))
+    idx = sample_with_extremes(offsets, 64, 9)
+    assert np.array_equal(bits(got[idx]), bits(OracleProfile("1400").score_batch(*subset(codes, offsets, idx),
+                                                                                  threads=ORACLE_THREADS)))
+    multi.close()
+    with pytest.raises(MSVError):
+        msv.MultiGPU([engines[0], engines[0]])
+    for e in engines:
+        e.close()
