@@ -1,5 +1,6 @@
-# Full measurement pass for one round: bench lines (cfg3 default + cfg2/cfg5), the rocprofv3
-# kernel-trace/stats summaries of the cfg3 and cfg5 bench commands, and the PMC passes for both.
+# Full measurement pass for one round: bench lines (cfg3 default + cfg2/cfg4/cfg5), the rocprofv3
+# kernel-trace/stats summaries of the cfg3 and cfg5 bench commands (and the timed window of each),
+# and the PMC passes for cfg3 and cfg2.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 M=gpurun_out/measure
@@ -7,9 +8,10 @@ mkdir -p $M
 timeout -k 10 300 python bench.py > $M/bench_cfg3.json 2> $M/bench_cfg3.err
 timeout -k 10 300 python bench.py --config cfg2 > $M/bench_cfg2.json 2> $M/bench_cfg2.err
 timeout -k 10 300 python bench.py --config cfg5 --steps 5 > $M/bench_cfg5.json 2> $M/bench_cfg5.err
+timeout -k 10 400 python bench.py --config cfg4 --steps 10 > $M/bench_cfg4.json 2> $M/bench_cfg4.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $M/rocprof_bench -o run -- python3 bench.py --no-cpu > $M/bench_under_rocprof.json 2>&1
-python3 tools/rocprof_window.py $M/rocprof_bench/run_kernel_trace.csv --skip 12 --take 20 > $M/rocprof_window.json
+python3 tools/rocprof_window.py $M/rocprof_bench/run_kernel_trace.csv --last 20 > $M/rocprof_window.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $M/rocprof_bench_cfg5 -o run -- python3 bench.py --no-cpu --config cfg5 --steps 5 > $M/bench_cfg5_under_rocprof.json 2>&1
-python3 tools/rocprof_window.py $M/rocprof_bench_cfg5/run_kernel_trace.csv --skip 12 --take 5 > $M/rocprof_window_cfg5.json
-timeout -k 10 900 bash tools/pmc.sh cfg5 $M/pmc_cfg5 > $M/pmc_cfg5.log 2>&1
+python3 tools/rocprof_window.py $M/rocprof_bench_cfg5/run_kernel_trace.csv --last 5 > $M/rocprof_window_cfg5.json
 timeout -k 10 900 bash tools/pmc.sh cfg3 $M/pmc_cfg3 > $M/pmc_cfg3.log 2>&1
+timeout -k 10 900 bash tools/pmc.sh cfg2 $M/pmc_cfg2 > $M/pmc_cfg2.log 2>&1
