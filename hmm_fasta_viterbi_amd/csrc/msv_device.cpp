@@ -227,7 +227,7 @@ struct msv_profile {
     std::vector<hipEvent_t> events;
     uint64_t* h_off = nullptr;
     size_t h_off_cap = 0;
-    uint32_t pipe_first_den = 8, pipe_growth = 3;  // piece sizes: total / first_den, then x growth
+    uint32_t pipe_first_den = 5, pipe_growth = 2;  // piece sizes: total / first_den, then x growth
     uint32_t pipe_streams = 2;                      // compute streams the pieces alternate over
     // msv_score_batch_async: kAsyncSlots staging sets, so the H2D of one call runs under the kernel
     // of the call before it
@@ -760,11 +760,11 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p->stream;
 
     // Copy/compute pipeline.  The batch is cut into pieces (contiguous sequence ranges) whose
-    // residue counts grow geometrically from ~1/8 of the batch (x3: 3 pieces for cfg3, the best plan
+    // residue counts grow geometrically from 1/5 of the batch (x2: 3 pieces for cfg3, the best plan
     // in tools/host_pipeline_sweep.py, profiles/r02_host_pipeline_sweep.jsonl), so the first kernel
     // starts after a short copy and every later piece's H2D (copy stream) runs under the kernels of
-    // the pieces before it.  Piece k's offsets are rebased and sent right before its residues, and
-    // its longest-first order waits only for those offsets.  Pieces alternate between two compute
+    // the pieces before it.  All offsets go first, and every piece's longest-first order runs before
+    // the first kernel (under piece 0's residue copy).  Pieces alternate between two compute
     // streams, so a piece's kernel fills the CUs that the previous piece's drain tail frees (each
     // launch has its own dequeue counter slot).  Scores and the error word come back once at the end
     // (pageable destinations would make per-piece D2H copies block the host thread that enqueues the
@@ -790,46 +790,57 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         if (!p->copy_stream) MSV_HIP(hipStreamCreateWithFlags(&p->copy_stream, hipStreamNonBlocking));
         cs[1] = p->pipe_streams == 2 ? p->stream2 : st;
         cp = p->copy_stream;
-        while (p->events.size() < 2 * P + 2) {
+        while (p->events.size() < P + 4) {
             hipEvent_t e = nullptr;
             MSV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice));
             p->events.push_back(e);
         }
         // fork: both helper streams start after the caller's stream's earlier work
-        MSV_HIP(hipEventRecord(p->events[2 * P], st));
-        MSV_HIP(hipStreamWaitEvent(cp, p->events[2 * P], 0));
-        MSV_HIP(hipStreamWaitEvent(cs[1], p->events[2 * P], 0));
+        MSV_HIP(hipEventRecord(p->events[P + 2], st));
+        MSV_HIP(hipStreamWaitEvent(cp, p->events[P + 2], 0));
+        MSV_HIP(hipStreamWaitEvent(cs[1], p->events[P + 2], 0));
+    }
+    // 1. every piece's offsets (rebased on the piece's first residue, at h_off[cut[k] + k ..]) in ONE
+    //    H2D, then the piece residues in order, all on the copy stream
+    for (size_t k = 0; k < P; ++k) {
+        uint64_t* ho = p->h_off + cut[k] + k;
+        const uint64_t base = offsets[cut[k]], cn = cut[k + 1] - cut[k];
+        for (uint64_t i = 0; i <= cn; ++i) ho[i] = offsets[cut[k] + i] - base;
+    }
+    MSV_HIP(hipMemcpyAsync(p->d_off, p->h_off, (n + P) * sizeof(uint64_t), hipMemcpyHostToDevice, cp));
+    if (pipe) {
+        MSV_HIP(hipEventRecord(p->events[0], cp));  // offsets landed
+        MSV_HIP(hipStreamWaitEvent(st, p->events[0], 0));
     }
     const uint64_t base0 = offsets[0];
     for (size_t k = 0; k < P; ++k) {
         const uint64_t lo = offsets[cut[k]] - base0, bytes = offsets[cut[k + 1]] - offsets[cut[k]];
-        const uint64_t cn = cut[k + 1] - cut[k];
-        // piece k's offsets, rebased on its first residue, at h_off[cut[k] + k .. cut[k+1] + k]
-        uint64_t* ho = p->h_off + cut[k] + k;
-        const uint64_t base = offsets[cut[k]];
-        for (uint64_t i = 0; i <= cn; ++i) ho[i] = offsets[cut[k] + i] - base;
-        uint64_t* d_off = p->d_off + cut[k] + k;
-        hipStream_t c = cs[k & 1];
-        MSV_HIP(hipMemcpyAsync(d_off, ho, (cn + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, cp));
-        if (pipe) {
-            MSV_HIP(hipEventRecord(p->events[2 * k], cp));
-            MSV_HIP(hipStreamWaitEvent(c, p->events[2 * k], 0));
-        }
         if (bytes) MSV_HIP(hipMemcpyAsync(p->d_res + lo, residues + base0 + lo, bytes, hipMemcpyHostToDevice, cp));
-        // longest-first dequeue order of the piece (shorter drain tail; ~15-20% on 100k sequences)
-        s = msv_order_longest_first(p, d_off, cn, p->d_order + cut[k], c);
+        if (pipe) MSV_HIP(hipEventRecord(p->events[2 + k], cp));  // piece k's residues landed
+    }
+    // 2. every piece's longest-first order up front on the caller's stream, while piece 0's residues
+    //    are still in flight: an order kernel enqueued behind a running MSV kernel would find no free
+    //    VGPRs until that kernel's blocks drain, delaying the next piece's launch
+    for (size_t k = 0; k < P; ++k) {
+        s = msv_order_longest_first(p, p->d_off + cut[k] + k, cut[k + 1] - cut[k], p->d_order + cut[k], st);
         if (s != MSV_OK) return s;
-        if (pipe) {
-            MSV_HIP(hipEventRecord(p->events[2 * k + 1], cp));
-            MSV_HIP(hipStreamWaitEvent(c, p->events[2 * k + 1], 0));
-        }
-        s = launch_batch(p, bytes ? p->d_res + lo : p->d_dummy, std::max<uint64_t>(bytes, 1), d_off, cn,
-                         p->d_order + cut[k], p->d_scores + cut[k], c, !pipe);
+    }
+    if (pipe) {
+        MSV_HIP(hipEventRecord(p->events[1], st));  // orders done
+        MSV_HIP(hipStreamWaitEvent(cs[1], p->events[1], 0));
+    }
+    // 3. the kernels, alternating over the compute streams, each after its piece's residues
+    for (size_t k = 0; k < P; ++k) {
+        const uint64_t lo = offsets[cut[k]] - base0, bytes = offsets[cut[k + 1]] - offsets[cut[k]];
+        hipStream_t c = cs[k & 1];
+        if (pipe) MSV_HIP(hipStreamWaitEvent(c, p->events[2 + k], 0));
+        s = launch_batch(p, bytes ? p->d_res + lo : p->d_dummy, std::max<uint64_t>(bytes, 1), p->d_off + cut[k] + k,
+                         cut[k + 1] - cut[k], p->d_order + cut[k], p->d_scores + cut[k], c, !pipe);
         if (s != MSV_OK) return s;
     }
     if (pipe) {  // join the second compute stream back into the caller's
-        MSV_HIP(hipEventRecord(p->events[2 * P + 1], cs[1]));
-        MSV_HIP(hipStreamWaitEvent(st, p->events[2 * P + 1], 0));
+        MSV_HIP(hipEventRecord(p->events[P + 3], cs[1]));
+        MSV_HIP(hipStreamWaitEvent(st, p->events[P + 3], 0));
     }
     MSV_HIP(hipMemcpyAsync(scores, p->d_scores, n * sizeof(float), hipMemcpyDeviceToHost, st));
     MSV_HIP(hipMemcpyAsync(h_err, p->d_words + kErrWord, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -880,12 +891,15 @@ msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const 
     // copy stream: this call's inputs (they overlap the previous call's kernel on the compute stream)
     MSV_HIP(hipMemcpyAsync(a.d_off, a.h_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, cp));
     if (total) MSV_HIP(hipMemcpyAsync(a.d_res, residues + base, total, hipMemcpyHostToDevice, cp));
+    // the order right behind the copy (it runs in the previous call's drain tail, not after it)
+    if (n) {
+        s = msv_order_longest_first(p, a.d_off, n, a.d_ord, cp);
+        if (s != MSV_OK) return s;
+    }
     MSV_HIP(hipEventRecord(a.copied, cp));
-    // compute stream: order, kernel, scores and the slot's error word back to the host
+    // compute stream: kernel, scores and the slot's error word back to the host
     MSV_HIP(hipStreamWaitEvent(cs, a.copied, 0));
     if (n) {
-        s = msv_order_longest_first(p, a.d_off, n, a.d_ord, cs);
-        if (s != MSV_OK) return s;
         s = launch_batch(p, total ? a.d_res : p->d_dummy, std::max<uint64_t>(total, 1), a.d_off, n, a.d_ord, a.d_sc,
                          cs, true, d_err);
         if (s != MSV_OK) return s;

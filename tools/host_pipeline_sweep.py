@@ -36,7 +36,7 @@ def main():
     pinned = torch.from_numpy(codes).pin_memory().numpy()
     L = _native.lib()
     L.msv_debug_set_pipeline.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32]
-    plans = [(0, 2, 1), (8, 3, 2), (8, 3, 1), (6, 2, 2), (6, 2, 1), (5, 2, 2), (7, 2, 2)]
+    plans = [(0, 2, 1), (5, 2, 2), (4, 2, 2), (6, 2, 2), (8, 3, 2), (3, 2, 2), (5, 3, 2)]
     res = int(offsets[-1])
     want = e.score_batch(codes=codes, offsets=offsets)
     for _ in range(10):  # clock ramp
