@@ -227,7 +227,7 @@ struct msv_profile {
     std::vector<hipEvent_t> events;
     uint64_t* h_off = nullptr;
     size_t h_off_cap = 0;
-    uint32_t pipe_first_den = 5, pipe_growth = 2;  // piece sizes: total / first_den, then x growth
+    uint32_t pipe_first_den = 4, pipe_growth = 2;  // piece sizes: total / first_den, then x growth
     uint32_t pipe_streams = 2;                      // compute streams the pieces alternate over
     // msv_score_batch_async: kAsyncSlots staging sets, so the H2D of one call runs under the kernel
     // of the call before it
@@ -760,7 +760,7 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p->stream;
 
     // Copy/compute pipeline.  The batch is cut into pieces (contiguous sequence ranges) whose
-    // residue counts grow geometrically from 1/5 of the batch (x2: 3 pieces for cfg3, the best plan
+    // residue counts grow geometrically from 1/4 of the batch (x2: 2 pieces for cfg3, the best plan
     // in tools/host_pipeline_sweep.py, profiles/r02_host_pipeline_sweep.jsonl), so the first kernel
     // starts after a short copy and every later piece's H2D (copy stream) runs under the kernels of
     // the pieces before it.  All offsets go first, and every piece's longest-first order runs before
