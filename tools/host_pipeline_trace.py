@@ -1,0 +1,42 @@
+"""Timeline of msv_score_batch's host pipeline for rocprofv3 --kernel-trace --memory-copy-trace:
+`--calls` warm calls of one config's batch from pinned memory, the last `--mark` of them after a
+1 ms host sleep so they stand apart in the trace.
+
+    rocprofv3 --kernel-trace --memory-copy-trace -d out -o run -- python3 tools/host_pipeline_trace.py
+    python3 tools/pipeline_timeline.py out/run_kernel_trace.csv out/run_memory_copy_trace.csv
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg3")
+    ap.add_argument("--calls", type=int, default=30)
+    ap.add_argument("--mark", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    import bench  # noqa: F401  (sets GPU_MAX_HW_QUEUES before HIP starts)
+    import hmm_fasta_viterbi_amd as msv
+    from hmm_fasta_viterbi_amd.synthetic import random_batch
+    prof, n, lmin, lmax, seed, _ = bench.CONFIGS[a.config]
+    e = msv.MSV_HMM(msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof)))
+    codes, offsets = random_batch(seed * 1000, n, lmin, lmax)
+    pinned = torch.from_numpy(codes).pin_memory().numpy()
+    for k in range(a.calls):
+        if k >= a.calls - a.mark:
+            time.sleep(0.001)
+        t = time.perf_counter()
+        e.score_batch(codes=pinned, offsets=offsets)
+        print(f"call {k}: {(time.perf_counter() - t) * 1e3:.3f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()
