@@ -281,21 +281,23 @@ def main():
     # Pinned = residues in page-locked memory (SURVEY 8(d)'s headline shape); pageable = plain numpy.
     pinned_codes = torch.from_numpy(codes).pin_memory().numpy()
 
-    def host_rate(src, settle_s=0.0):
+    def host_rate(src, out, settle_s=0.0):
         t = time.perf_counter()  # warm; the first call also settles the GPU clock (ramps from idle)
         while True:
-            engine.score_batch(codes=src, offsets=offsets)
+            engine.score_batch(codes=src, offsets=offsets, out=out)
             if time.perf_counter() - t >= settle_s:
                 break
         for _ in range(3):
-            engine.score_batch(codes=src, offsets=offsets)
+            engine.score_batch(codes=src, offsets=offsets, out=out)
         t = time.perf_counter()
         for _ in range(args.steps):
-            out = engine.score_batch(codes=src, offsets=offsets)
-        return residues * args.steps / (time.perf_counter() - t) / 1e6, out
+            engine.score_batch(codes=src, offsets=offsets, out=out)
+        return residues * args.steps / (time.perf_counter() - t) / 1e6, out.copy()
 
-    host_pinned, pinned_scores = host_rate(pinned_codes, settle_s=0.5)
-    host_pageable, pageable_scores = host_rate(codes)
+    # pinned: residues AND scores in page-locked host memory; pageable: both plain numpy arrays
+    host_pinned, pinned_scores = host_rate(pinned_codes, torch.empty(n, dtype=torch.float32).pin_memory().numpy(),
+                                           settle_s=0.5)
+    host_pageable, pageable_scores = host_rate(codes, np.zeros(n, np.float32))
 
     # Stream of batches (serving): msv_score_batch_async keeps two calls in flight, so each call's H2D
     # runs under the previous call's kernel; scores land in pinned host arrays.

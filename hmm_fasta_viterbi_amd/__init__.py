@@ -173,13 +173,18 @@ class MSV_HMM:
 
     # -- batch API --------------------------------------------------------------------------
     def score_batch(self, seqs: Sequence[str] | None = None, *, codes: np.ndarray | None = None,
-                    offsets: np.ndarray | None = None) -> np.ndarray:
+                    offsets: np.ndarray | None = None, out: np.ndarray | None = None) -> np.ndarray:
+        """Scores of a host batch (msv_score_batch).  `out`: optional float32[n] destination (e.g. a
+        pinned array, torch pin_memory().numpy(), so the scores' D2H needs no runtime staging)."""
         if seqs is not None:
             codes, offsets = pack_sequences(seqs)
         codes = np.ascontiguousarray(codes, np.uint8)
         offsets = np.ascontiguousarray(offsets, np.uint64)
         n = len(offsets) - 1
-        out = np.zeros(n, np.float32)
+        if out is None:
+            out = np.zeros(n, np.float32)
+        elif out.dtype != np.float32 or out.shape != (n,) or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous float32 array of n scores")
         st = _native.lib().msv_score_batch(self._p, codes.ctypes.data if codes.size else None, offsets.ctypes.data,
                                            n, out.ctypes.data, None)
         if st == _native.MSV_ERR_BAD_RESIDUE:

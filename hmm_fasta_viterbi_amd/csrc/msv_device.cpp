@@ -800,45 +800,42 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         MSV_HIP(hipStreamWaitEvent(cp, p->events[P + 2], 0));
         MSV_HIP(hipStreamWaitEvent(cs[1], p->events[P + 2], 0));
     }
-    // 1. every piece's offsets (rebased on the piece's first residue, at h_off[cut[k] + k ..]) in ONE
-    //    H2D, then the piece residues in order, all on the copy stream
-    for (size_t k = 0; k < P; ++k) {
-        uint64_t* ho = p->h_off + cut[k] + k;
-        const uint64_t base = offsets[cut[k]], cn = cut[k + 1] - cut[k];
-        for (uint64_t i = 0; i <= cn; ++i) ho[i] = offsets[cut[k] + i] - base;
-    }
-    MSV_HIP(hipMemcpyAsync(p->d_off, p->h_off, (n + P) * sizeof(uint64_t), hipMemcpyHostToDevice, cp));
-    if (pipe) {
-        MSV_HIP(hipEventRecord(p->events[0], cp));  // offsets landed
-        MSV_HIP(hipStreamWaitEvent(st, p->events[0], 0));
-    }
+    // 1. the residue pieces go first, in order, on the copy stream: their DMA is the critical path
     const uint64_t base0 = offsets[0];
     for (size_t k = 0; k < P; ++k) {
         const uint64_t lo = offsets[cut[k]] - base0, bytes = offsets[cut[k + 1]] - offsets[cut[k]];
         if (bytes) MSV_HIP(hipMemcpyAsync(p->d_res + lo, residues + base0 + lo, bytes, hipMemcpyHostToDevice, cp));
         if (pipe) MSV_HIP(hipEventRecord(p->events[2 + k], cp));  // piece k's residues landed
     }
-    // 2. every piece's longest-first order up front on the caller's stream, while piece 0's residues
-    //    are still in flight: an order kernel enqueued behind a running MSV kernel would find no free
-    //    VGPRs until that kernel's blocks drain, delaying the next piece's launch
+    // 2. meanwhile every piece's offsets (rebased on the piece's first residue, at h_off[cut[k] + k ..])
+    //    in ONE H2D on the caller's stream, then every piece's longest-first order there, under the
+    //    first residue copy (an order kernel enqueued behind a running MSV kernel would find no free
+    //    VGPRs until that kernel's blocks drain, delaying the next piece's launch)
+    for (size_t k = 0; k < P; ++k) {
+        uint64_t* ho = p->h_off + cut[k] + k;
+        const uint64_t base = offsets[cut[k]], cn = cut[k + 1] - cut[k];
+        for (uint64_t i = 0; i <= cn; ++i) ho[i] = offsets[cut[k] + i] - base;
+    }
+    MSV_HIP(hipMemcpyAsync(p->d_off, p->h_off, (n + P) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     for (size_t k = 0; k < P; ++k) {
         s = msv_order_longest_first(p, p->d_off + cut[k] + k, cut[k + 1] - cut[k], p->d_order + cut[k], st);
         if (s != MSV_OK) return s;
     }
     if (pipe) {
-        MSV_HIP(hipEventRecord(p->events[1], st));  // orders done
+        MSV_HIP(hipEventRecord(p->events[1], st));  // offsets and orders done
         MSV_HIP(hipStreamWaitEvent(cs[1], p->events[1], 0));
     }
-    // 3. the kernels, alternating over the compute streams, each after its piece's residues
+    // 3. the kernels, alternating over the compute streams so that the LAST piece runs on the caller's
+    //    stream (the scores' D2H then waits on no other stream), each after its piece's residues
     for (size_t k = 0; k < P; ++k) {
         const uint64_t lo = offsets[cut[k]] - base0, bytes = offsets[cut[k + 1]] - offsets[cut[k]];
-        hipStream_t c = cs[k & 1];
+        hipStream_t c = cs[(P - 1 - k) & 1];
         if (pipe) MSV_HIP(hipStreamWaitEvent(c, p->events[2 + k], 0));
         s = launch_batch(p, bytes ? p->d_res + lo : p->d_dummy, std::max<uint64_t>(bytes, 1), p->d_off + cut[k] + k,
                          cut[k + 1] - cut[k], p->d_order + cut[k], p->d_scores + cut[k], c, !pipe);
         if (s != MSV_OK) return s;
     }
-    if (pipe) {  // join the second compute stream back into the caller's
+    if (pipe) {  // join the second compute stream (done before the last piece) back into the caller's
         MSV_HIP(hipEventRecord(p->events[P + 3], cs[1]));
         MSV_HIP(hipStreamWaitEvent(st, p->events[P + 3], 0));
     }

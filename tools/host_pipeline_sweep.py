@@ -34,9 +34,10 @@ def main():
     e = msv.MSV_HMM(msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof)))
     codes, offsets = random_batch(seed * 1000, n, lmin, lmax)
     pinned = torch.from_numpy(codes).pin_memory().numpy()
+    pout = torch.empty(n, dtype=torch.float32).pin_memory().numpy()
     L = _native.lib()
     L.msv_debug_set_pipeline.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32]
-    plans = [(0, 2, 1), (5, 2, 2), (4, 2, 2), (6, 2, 2), (8, 3, 2), (3, 2, 2), (5, 3, 2)]
+    plans = [(0, 2, 1), (4, 2, 2), (5, 2, 2), (6, 2, 2), (8, 2, 2), (6, 3, 2), (8, 3, 2), (3, 2, 2)]
     res = int(offsets[-1])
     want = e.score_batch(codes=codes, offsets=offsets)
     for _ in range(10):  # clock ramp
@@ -45,10 +46,10 @@ def main():
         for den, g, ns in plans:
             assert L.msv_debug_set_pipeline(e._p, den, g, ns) == 0
             for _ in range(2):
-                e.score_batch(codes=pinned, offsets=offsets)
+                e.score_batch(codes=pinned, offsets=offsets, out=pout)
             t = time.perf_counter()
             for _ in range(a.calls):
-                out = e.score_batch(codes=pinned, offsets=offsets)
+                out = e.score_batch(codes=pinned, offsets=offsets, out=pout).copy()
             ms = (time.perf_counter() - t) / a.calls * 1e3
             ok = bool(np.array_equal(out.view(np.uint32), want.view(np.uint32)))
             print(json.dumps({"config": a.config, "round": r, "first_den": den, "growth": g, "streams": ns, "ms": round(ms, 4),
