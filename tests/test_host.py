@@ -288,3 +288,31 @@ def test_native_random_fasta_generator_format(tmp_path):
     fa = msv.FASTA_protein_sequences(c)
     lens = np.diff(fa.offsets.astype(np.int64))
     assert len(fa) == 500 and fa.rejected == 0 and lens.min() >= 0 and lens.max() <= 900
+
+
+def test_msv_pvalues_gumbel_against_scipy():
+    """The Gumbel survival step of the P-values, pinned against an independent implementation
+    (scipy.stats.gumbel_r.sf with loc = mu, scale = 1/lambda, HMMER's esl_gumbel_surv in closed
+    form), on the bit scores the null1 step gives (HMMER3's p7_bg_NullOne restated; no reference
+    implementation exists, so that step stays unpinned)."""
+    import scipy.stats as ss
+    from hmm_fasta_viterbi_amd import _native
+    rng = np.random.default_rng(7)
+    n = 4000
+    lengths = rng.integers(1, 3000, n).astype(np.uint64)
+    offsets = np.zeros(n + 1, np.uint64)
+    np.cumsum(lengths, out=offsets[1:])
+    scores = rng.uniform(-40.0, 25.0, n).astype(np.float32)
+    for prof in ("100.hmm", "1400.hmm", "2405.hmm"):
+        h = msv.Profile_HMM(profile_path(prof))
+        mu, lam = h.stats_local_msv_mu, h.stats_local_msv_lambda
+        out = np.zeros(n, np.float64)
+        assert _native.lib().msv_pvalues(scores.ctypes.data, offsets.ctypes.data, n, mu, lam, out.ctypes.data) == 0
+        L = lengths.astype(np.float64)
+        p1 = (lengths.astype(np.float32) / (lengths + 1).astype(np.float32)).astype(np.float32)
+        nullsc = (L * np.log(p1.astype(np.float64)) + np.log(1.0 - p1.astype(np.float64))).astype(np.float32)
+        bits = ((scores - nullsc).astype(np.float32) / np.float32(0.69314718055994529)).astype(np.float32)
+        want = ss.gumbel_r.sf(bits.astype(np.float64), loc=np.float64(mu), scale=1.0 / np.float64(lam))
+        # scipy's sf = -expm1(-exp(-y)); the library's 1 - exp(-exp(-y)) loses relative precision only
+        # where P is tiny, which the small-tail branch (P = exp(-y) when exp(-y) < 5e-9) covers
+        np.testing.assert_allclose(out, want, rtol=1e-7, atol=1e-15)
