@@ -450,6 +450,9 @@ msv_status msv_hmm_msv_scores(const msv_hmm* hmm, float* emission_scores, float*
 void msv_profile_destroy(msv_profile* p) {
     if (!p) return;
     DeviceGuard g(p->device);
+    // work still queued on any stream (an unwaited msv_score_batch_async call, a device call on the
+    // caller's stream) may use the buffers and pinned staging freed below
+    (void)hipDeviceSynchronize();
     (void)hipFree(p->main.d_etab);
     (void)hipFree(p->lat.d_etab);
     (void)hipFree(p->d_lentab);
@@ -785,6 +788,19 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     uint32_t* h_err = reinterpret_cast<uint32_t*>(p->h_off + n + P);
     const bool pipe = P > 1;
     hipStream_t cs[2] = {st, st}, cp = st;
+    // On an early error return, copies reading the pinned h_off (rewritten by the next call) and
+    // kernels writing the staging buffers may still be queued: drain every stream used first.
+    struct Drain {
+        hipStream_t* cs;
+        hipStream_t* cp;
+        bool armed = true;
+        ~Drain() {
+            if (!armed) return;
+            (void)hipStreamSynchronize(cs[0]);
+            (void)hipStreamSynchronize(cs[1]);
+            (void)hipStreamSynchronize(*cp);
+        }
+    } drain{cs, &cp};
     if (pipe) {
         if (!p->stream2) MSV_HIP(hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking));
         if (!p->copy_stream) MSV_HIP(hipStreamCreateWithFlags(&p->copy_stream, hipStreamNonBlocking));
@@ -842,6 +858,7 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     MSV_HIP(hipMemcpyAsync(scores, p->d_scores, n * sizeof(float), hipMemcpyDeviceToHost, st));
     MSV_HIP(hipMemcpyAsync(h_err, p->d_words + kErrWord, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     MSV_HIP(hipStreamSynchronize(st));  // also: the pinned h_off is rewritten by the next call
+    drain.armed = false;
     if (*h_err == 0) return MSV_OK;
     return msv_profile_check(p, st);  // reads, clears and reports the latched error bits
 }
