@@ -96,6 +96,13 @@ __device__ __forceinline__ float dpp_perm(float src) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(src), CTRL, 0xF, 0xF, true));
 }
 
+// Lane q of each 16-lane DPP row, broadcast to the whole row (row_newbcast, gfx90a+).
+template <int Q>
+__device__ __forceinline__ uint32_t row_bcast_lane(uint32_t v) {
+    static_assert(Q >= 0 && Q < 16, "row_newbcast lane");
+    return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0x150 + Q, 0xF, 0xF, true));
+}
+
 // Max over the G lanes of a group, result in every lane of the group.
 template <int G>
 __device__ __forceinline__ float group_max(float x) {
@@ -161,6 +168,9 @@ struct Stream {
     uint32_t pos, endpos, endp, ev, seq;
     uint8_t r[RPF];   // residue codes of the next RPF rows (bytes: a 32-bit slot made the compiler
                       // zero-extend each load where it lands, i.e. wait for it in the same row)
+    uint32_t cur;     // BLK: residue blocks, lane b of each 16-lane DPP row = the row of phase b
+    uint8_t nxt;      // (cur: this 16-row block, clamped to the poison row; nxt: the next one, raw --
+                      // a byte for the reason above, so its load is waited for only where it is used)
     bool active;
     bool junk;        // current "sequence" is an empty/too-long record: discard its row
 };
@@ -194,6 +204,22 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     constexpr int ROW_F4 = CA * G;           // float4 per LDS residue row
     constexpr int HBP = (HB + 1) & ~1;       // SPLIT: halves per lane in the B table (padded to even)
     constexpr int LDS_ROWS = SPLIT ? kAminoAcids : lds_rows_for(G, S);
+    // Residue slots rotate instead of shifting (ROT): the row of phase P reads its residue from
+    // r[P] and loads the residue RPF rows ahead into the same slot, and the main loop is unrolled
+    // over the RPF phases.  A shift register moves every prefetched byte once per row, and a move of
+    // a register with a load in flight waits for that load (s_waitcnt vmcnt(0) in every row): the
+    // short rows of small profiles then last as long as one L2 round trip.  Paths that keep the
+    // shift: one residue of prefetch (nothing to shift), the G = 64 row-class layout and D = 2.
+    constexpr bool ROT = !BIG && D == 1 && St::RPF > 1;
+    // Residue BLOCKS (BLK, short rows with G >= 16): instead of one byte load per row, every lane
+    // loads one byte of a 16-row block (lane b of each DPP row: the row of phase b), once per 16
+    // rows, a block ahead; a row takes its residue with one row_newbcast DPP move.  The row loop is
+    // unrolled over the 16 phases and the block in flight is consumed 14-16 rows after its load, so
+    // the waits the compiler places at the loop header or after a rare path (which merge every load
+    // in flight: with per-row slots the header waited for the load of the row before, once per RPF
+    // rows -- the bound of cfg2's 100.hmm rows) find it landed.  16x fewer VMEM instructions.
+    constexpr bool BLK = ROT && G >= 16 && !SPLIT;
+    constexpr int NPH = BLK ? 16 : St::RPF;  // phases of the unrolled row loop
     // Cross-row emission prefetch: when the ring holds a whole row (small profiles), the NEXT row's
     // chunks are requested right after this row's last cell update, so the LDS latency hides behind
     // the E butterfly and the specials instead of stalling the start of every row.
@@ -205,7 +231,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
 #ifndef MSV_XROW_DEPTH
 #define MSV_XROW_DEPTH 2
 #endif
-    constexpr bool XROW2 = XROW && MSV_XROW_DEPTH == 2 && St::RPF % 2 == 0 && PF <= 2;  // +4 PF VGPRs
+    constexpr bool XROW2 = XROW && MSV_XROW_DEPTH == 2 && NPH % 2 == 0 && PF <= 2;  // +4 PF VGPRs
     static_assert(SPLIT || BIG == (LDS_ROWS < kTableRows), "BIG <=> table does not fit LDS");
     __shared__ float4 tab[LDS_ROWS * ROW_F4];
 
@@ -230,18 +256,12 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     constexpr uint32_t kNone = 0xFFFFFFFFu;
     uint32_t pending = kNone;
 
-    // Residue slots rotate instead of shifting (ROT): the row of phase P reads its residue from
-    // r[P] and loads the residue RPF rows ahead into the same slot, and the main loop is unrolled
-    // over the RPF phases.  A shift register moves every prefetched byte once per row, and a move of
-    // a register with a load in flight waits for that load (s_waitcnt vmcnt(0) in every row): the
-    // short rows of small profiles then last as long as one L2 round trip.  Paths that keep the
-    // shift: one residue of prefetch (nothing to shift), the G = 64 row-class layout and D = 2.
-    constexpr bool ROT = !BIG && D == 1 && St::RPF > 1;
     using Ph0 = std::integral_constant<int, 0>;
+    const uint32_t blk_lane = static_cast<uint32_t>(gl & 15);  // BLK: the lane's row within a block
 
     // Start the next non-empty sequence in a stream (or retire the stream); `ph` is the phase of the
     // row that will run next (its residue goes to slot r[ph]).
-    auto begin = [&](St& st, auto ph) {
+    auto begin = [&](St& st, auto ph) __attribute__((always_inline)) {
         constexpr int PH = decltype(ph)::value;
         // Loop-free on purpose: a retry loop around the group broadcast here was unswitched by
         // the compiler into per-lane copies (see group_take).  An empty (or too long) record
@@ -287,8 +307,32 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         st.B = st.move;   // dp[0][B] = tr_move (MSV_HMM.cpp:97)
         st.active = !retire;
         st.junk = !run;
+        if constexpr (BLK) {
+            // The first row runs at phase PH: cur lane b (b >= PH) = residue pos + b - PH, nxt lane b =
+            // pos + 16 + b - PH.  PH = 0: the phase-0 row first moves nxt into cur, so both hold the
+            // first block.  (Lanes below PH are never read; max() keeps their index >= pos.)
+            const uint32_t ic = max(st.pos + blk_lane, st.pos + PH) - PH;
+            const uint32_t in = PH == 0 ? ic : st.pos + blk_lane + (16 - PH);
+            st.cur = min(static_cast<uint32_t>(res[min(ic, st.endpos)]), static_cast<uint32_t>(kPoisonRow));
+            st.nxt = res[min(in, st.endpos)];
+        } else {
 #pragma unroll
-        for (int q = 0; q < St::RPF; ++q) st.r[(PH + q) % St::RPF] = res[min(st.pos + q, st.endpos)];
+            for (int q = 0; q < St::RPF; ++q) st.r[(PH + q) % St::RPF] = res[min(st.pos + q, st.endpos)];
+        }
+    };
+    // Residue code of the row at phase P (0 <= P < NPH + 2) for a row of phase <= P: BLK reads it from
+    // the blocks (clamped to the poison row); otherwise the slot (clamped where the row address is made).
+    auto resid = [&](St& st, auto pp) __attribute__((always_inline)) -> uint32_t {
+        constexpr int P = decltype(pp)::value;
+        if constexpr (BLK) {
+            if constexpr (P < 16) {
+                return row_bcast_lane<P>(st.cur);
+            } else {
+                return min(row_bcast_lane<P - 16>(static_cast<uint32_t>(st.nxt)), static_cast<uint32_t>(kPoisonRow));
+            }
+        } else {
+            return st.r[P % St::RPF];
+        }
     };
     auto init = [&](St& st) {
         st.nbr = NINF;
@@ -304,7 +348,8 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // rr * ROW_F4 + gl compiled to v_mul_u32_u24 + v_or: profiles/r01_ab_row_address.jsonl).
     const uint32_t lds_lane = static_cast<uint32_t>(gl * 16);
     auto lds_row = [&](uint32_t r) -> const float4* {
-        const uint32_t rr = min(r, static_cast<uint32_t>(SPLIT ? kAminoAcids - 1 : kPoisonRow));
+        // (BLK residues arrive clamped)
+        const uint32_t rr = BLK ? r : min(r, static_cast<uint32_t>(SPLIT ? kAminoAcids - 1 : kPoisonRow));
         uint32_t off;
         asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(off) : "v"(rr), "s"(static_cast<uint32_t>(ROW_F4 * 16)), "v"(lds_lane));
         return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(tab) + off);
@@ -334,7 +379,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     };
     auto row_ptr = [&](St& st, auto ph) -> const float4* {
         if constexpr (!BIG) {
-            return lds_row(st.r[decltype(ph)::value]);
+            return lds_row(resid(st, ph));
         } else {
             const uint32_t rr = min(st.r[0], static_cast<uint32_t>(kPoisonRow));
             return (rr < static_cast<uint32_t>(LDS_ROWS)) ? &tab[rr * ROW_F4 + gl] : &a.etab[rr * ROW_F4 + gl];
@@ -348,7 +393,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     };
     auto prologue = [&](St& st, auto& rc, const float4* ep, auto ph) {
         (void)ph;
-        rc.rnext = res[min(st.pos + St::RPF, st.endpos)];
+        if constexpr (!BLK) rc.rnext = res[min(st.pos + St::RPF, st.endpos)];
         rc.ep = ep;
         rc.Bt = st.B + trBMk;
         if constexpr (G >= 16) {
@@ -476,7 +521,9 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         st.B = st.N + st.move;
         if (__builtin_expect(__any(st.J >= st.N), 0)) st.B = fmaxf(st.N, group_max<G>(st.J)) + st.move;
         ++st.pos;
-        if constexpr (ROT) {
+        if constexpr (BLK) {
+            // the blocks advance once per 16 rows (step, phase 0)
+        } else if constexpr (ROT) {
             st.r[decltype(ph)::value] = rc.rnext;  // this row's slot now holds the row RPF ahead
         } else {
 #pragma unroll
@@ -485,7 +532,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         }
     };
     // `ph`: phase of the row that runs next.
-    auto finish = [&](St& st, auto ph) {
+    auto finish = [&](St& st, auto ph) __attribute__((always_inline)) {
         // Every lane of the group is here (pos == endp is group-uniform), so the group reduction of
         // the C partials reads only active lanes of the same group.
         // (the copy of J is opaque so the compiler cannot hoist this select into every row)
@@ -515,7 +562,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
 
     RowCtx<PF> xr, xr1;  // XROW: the ring persists across rows (XROW2: xr for even phases, xr1 for odd)
     if constexpr (XROW) fill_ring(xr, row_ptr(s0, Ph0{}));
-    if constexpr (XROW2) fill_ring(xr1, lds_row(s0.r[1]));
+    if constexpr (XROW2) fill_ring(xr1, lds_row(resid(s0, std::integral_constant<int, 1>{})));
     fill_b(s0.r[0]);
 
     // slot of the residue of the row after a row of phase P
@@ -544,26 +591,31 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
 
     // One row of phase P of the single-stream, non-row-class paths (XROW or plain), then its events.
     // Returns whether the wave still has work.
-    auto step = [&](auto ph) -> bool {
+    auto step = [&](auto ph) __attribute__((always_inline)) -> bool {  // always_inline: 16 BLK phases exceed the inliner's budget
         constexpr int PH = decltype(ph)::value;
-        constexpr int PN = (PH + 1) % St::RPF;
+        constexpr int PN = (PH + 1) % NPH;
         using PhN = std::integral_constant<int, PN>;
+        if constexpr (BLK && PH == 0) {
+            // a new 16-row block: the one loaded 16 rows ago becomes current, the next is requested
+            s0.cur = min(static_cast<uint32_t>(s0.nxt), static_cast<uint32_t>(kPoisonRow));
+            s0.nxt = res[min(s0.pos + 16 + blk_lane, s0.endpos)];
+        }
         if constexpr (XROW2) {
             RowCtx<PF>& rc = (PH & 1) ? xr1 : xr;
             prologue(s0, rc, nullptr, ph);
             [&]<int... I>(std::integer_sequence<int, I...>) {
                 ((chunk(s0, rc, std::integral_constant<int, C4 - 1 - I>{})), ...);
             }(std::make_integer_sequence<int, C4>{});
-            // r[PH + 2] is the residue of the row after next (discarded if the sequence ends first)
-            fill_ring(rc, lds_row(s0.r[(PH + 2) % St::RPF]));
+            // the residue of the row after next (discarded if the sequence ends first)
+            fill_ring(rc, lds_row(resid(s0, std::integral_constant<int, PH + 2>{})));
             epilogue(s0, rc, ph);
         } else if constexpr (XROW) {
             prologue(s0, xr, nullptr, ph);
             [&]<int... I>(std::integer_sequence<int, I...>) {
                 ((chunk(s0, xr, std::integral_constant<int, C4 - 1 - I>{})), ...);
             }(std::make_integer_sequence<int, C4>{});
-            // r[PN] is the residue of the next row (discarded if this row ends the sequence)
-            fill_ring(xr, lds_row(s0.r[PN]));
+            // the residue of the next row (discarded if this row ends the sequence)
+            fill_ring(xr, lds_row(resid(s0, std::integral_constant<int, PH + 1>{})));
             epilogue(s0, xr, ph);
         } else {
             RowCtx<PF> c0;
@@ -579,11 +631,11 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
                 finish(s0, PhN{});
                 if constexpr (XROW2) {  // the new sequence's first two rows
                     fill_ring((PN & 1) ? xr1 : xr, row_ptr(s0, PhN{}));
-                    fill_ring((PN & 1) ? xr : xr1, lds_row(s0.r[(PN + 1) % St::RPF]));
+                    fill_ring((PN & 1) ? xr : xr1, lds_row(resid(s0, std::integral_constant<int, PN + 1>{})));
                 } else if constexpr (XROW) {
                     fill_ring(xr, row_ptr(s0, PhN{}));
                 }
-                fill_b(s0.r[PN]);
+                if constexpr (SPLIT) fill_b(s0.r[PN]);
             }
             live = __any(s0.active);
         }
@@ -593,10 +645,10 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
 
     while (live) {
         if constexpr (ROT) {
-            // RPF rows per iteration, one per residue slot; stops after any row that retires the wave
+            // NPH rows per iteration (residue slots, or the 16 rows of a BLK block); stops after any row that retires the wave
             [&]<int... I>(std::integer_sequence<int, I...>) {
                 (void)(step(std::integral_constant<int, I>{}) && ...);
-            }(std::make_integer_sequence<int, St::RPF>{});
+            }(std::make_integer_sequence<int, NPH>{});
         } else {
             if constexpr (BIG && G == 64) {
                 // One sequence per wave: the residue, hence the table row's home, is wave-uniform, so

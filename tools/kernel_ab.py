@@ -18,13 +18,16 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--warm", type=int, default=15)
     ap.add_argument("--time", type=int, default=20)
+    ap.add_argument("--profile", default="")
+    ap.add_argument("--n", type=int, default=0)
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     for r in range(a.rounds):
         for lib in a.libs:
             env = dict(os.environ, MSV_LIB_PATH=os.path.abspath(lib))
             out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "run_kernel.py"), "--config", a.config,
-                                  "--launches", str(a.warm), "--time", str(a.time)], env=env, capture_output=True,
+                                  "--launches", str(a.warm), "--time", str(a.time)]
+                                 + (["--profile", a.profile] if a.profile else []) + (["--n", str(a.n)] if a.n else []), env=env, capture_output=True,
                                  text=True, timeout=240, check=True).stdout.strip().splitlines()[-1]
             d = json.loads(out)
             d["round"] = r

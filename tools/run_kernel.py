@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--variant", default="")
     ap.add_argument("--no-order", action="store_true")
     ap.add_argument("--time", type=int, default=0)
+    ap.add_argument("--profile", default="", help="override the config's profile (e.g. 640.hmm)")
+    ap.add_argument("--n", type=int, default=0, help="override the config's sequence count")
     args = ap.parse_args()
     import torch
     import hmm_fasta_viterbi_amd as msv
@@ -29,6 +31,8 @@ def main():
     from bench import CONFIGS
 
     prof, n, lmin, lmax, seed = CONFIGS[args.config][:5]
+    prof = args.profile or prof
+    n = args.n or n
     eng = msv.MSV_HMM(msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof)))
     if args.variant:
         eng.set_variant(args.variant)
@@ -55,7 +59,7 @@ def main():
             b.record(st)
         eng.check(st.cuda_stream)
         ms = sorted(a.elapsed_time(b) for a, b in ev)
-        print(json.dumps({"config": args.config, "lib": os.environ.get("MSV_LIB_PATH", "in-tree"),
+        print(json.dumps({"config": args.config, "profile": prof, "n": n, "lib": os.environ.get("MSV_LIB_PATH", "in-tree"),
                           "variant": eng.describe()["variant"], "kernel_ms_mean": sum(ms) / len(ms),
                           "kernel_ms_median": ms[len(ms) // 2], "kernel_ms_min": ms[0]}), flush=True)
         return

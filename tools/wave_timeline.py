@@ -33,7 +33,7 @@ def main():
     L = _native.lib()
     L.msv_debug_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
     L.msv_debug_grid_waves.argtypes = [C.c_void_p]
-    prof, n, lmin, lmax, seed = CONFIGS[args.config]
+    prof, n, lmin, lmax, seed = CONFIGS[args.config][:5]
     n = args.n or n
     eng = msv.MSV_HMM(msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof)))
     if args.variant:
@@ -92,6 +92,8 @@ def main():
         "start_us_pct": q(start), "end_us_pct": q(end),
         "mean_wave_lifetime_frac": round(float(life.mean()), 4),
         "rows_per_wave_pct": q(rows),
+        "ns_per_row_pct": q((end - start) * 1000.0 / np.maximum(rows, 1)),
+        "waves_per_simd_pct": q(np.unique(cu_key * 4 + simd, return_counts=True)[1]),
         "end_us_by_xcc_median": {int(x): round(float(np.median(end[xcc == x])), 1) for x in sorted(set(xcc))},
         "end_us_by_xcc_max": {int(x): round(float(end[xcc == x].max()), 1) for x in sorted(set(xcc))},
     }
