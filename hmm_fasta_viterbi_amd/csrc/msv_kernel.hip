@@ -127,16 +127,18 @@ __device__ __forceinline__ uint32_t group_bcast(uint32_t v, int lane) {
     return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute((lane & ~(G - 1)) << 2, static_cast<int>(v)));
 }
 
-// Next sequence index for the whole group (one atomic by the group leader, broadcast).
+// Next sequence index for the whole group (one atomic by the group leader, broadcast).  Indices
+// below `first` (the grid's lane groups) are handed out statically: a group's first sequence is its
+// own group number, so a wave starts without an atomic round trip.
 // Branch-free on purpose: with `if (leader) v = atomicAdd(...)` the ROCm 7.2 optimiser unswitched
 // a loop containing this on `leader` into per-lane copies; the non-leader copy lost the atomic and
 // its ds_bpermute read a lane that was not executing (a launch that spun forever on index 0).
 // Every lane issues the atomic with increment leader ? 1 : 0; the wave-level atomic optimiser turns
 // that into one atomic per wave.
 template <int G>
-__device__ __forceinline__ uint32_t group_take(uint32_t* counter, bool leader, int lane) {
+__device__ __forceinline__ uint32_t group_take(uint32_t* counter, bool leader, int lane, uint32_t first) {
     const uint32_t v = atomicAdd(counter, leader ? 1u : 0u);
-    return group_bcast<G>(v, lane);
+    return group_bcast<G>(v, lane) + first;
 }
 
 }  // namespace
@@ -254,7 +256,9 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // half a sequence, and a batch smaller than twice the number of groups is still spread one
     // sequence per group instead of two per early group).
     constexpr uint32_t kNone = 0xFFFFFFFFu;
-    uint32_t pending = kNone;
+    const uint32_t n_groups = gridDim.x * (WAVES * 64 / G);  // statically assigned first indices
+    // the group's first sequence: its own group number (the first stream's begin consumes it)
+    uint32_t pending = (blockIdx.x * WAVES + (threadIdx.x >> 6)) * (64 / G) + static_cast<uint32_t>(lane / G);
 
     using Ph0 = std::integral_constant<int, 0>;
     const uint32_t blk_lane = static_cast<uint32_t>(gl & 15);  // BLK: the lane's row within a block
@@ -269,7 +273,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         // on neutral state and discarded, and the stream then restarts with the next index.
         uint32_t idx = pending;
         pending = kNone;
-        if (idx == kNone) idx = group_take<G>(a.counter, leader, lane);
+        if (idx == kNone) idx = group_take<G>(a.counter, leader, lane, n_groups);
         const bool retire = idx >= a.n;
         uint32_t s = 0;
         uint64_t o0 = 0, o1 = 0;
@@ -624,7 +628,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         // Events: see the generic loop below.
         if (G == 64 || __any(s0.pos == s0.ev)) {
             if (s0.pos == s0.ev && s0.ev != s0.endp) {
-                if (pending == kNone) pending = group_take<G>(a.counter, leader, lane);
+                if (pending == kNone) pending = group_take<G>(a.counter, leader, lane, n_groups);
                 s0.ev = s0.endp;
             }
             if (s0.pos == s0.endp) {
@@ -689,12 +693,12 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             // left out.)
             if (G == 64 || __any(D == 2 ? (s0.pos == s0.ev || s1.pos == s1.ev) : s0.pos == s0.ev)) {
                 if (s0.pos == s0.ev && s0.ev != s0.endp) {
-                    if (pending == kNone) pending = group_take<G>(a.counter, leader, lane);
+                    if (pending == kNone) pending = group_take<G>(a.counter, leader, lane, n_groups);
                     s0.ev = s0.endp;
                 }
                 if constexpr (D == 2) {
                     if (s1.pos == s1.ev && s1.ev != s1.endp) {
-                        if (pending == kNone) pending = group_take<G>(a.counter, leader, lane);
+                        if (pending == kNone) pending = group_take<G>(a.counter, leader, lane, n_groups);
                         s1.ev = s1.endp;
                     }
                 }
