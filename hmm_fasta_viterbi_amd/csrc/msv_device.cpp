@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -216,7 +217,8 @@ struct msv_profile {
     float2* d_lentab = nullptr;
     uint32_t lentab_n = 0;
     uint32_t* d_words = nullptr;  // kLaunchSlots x {dequeue counter, waves still running}, sticky error bits
-    uint32_t* d_hist = nullptr;   // kLaunchSlots longest-first counting-sort histograms
+    uint32_t* d_hist = nullptr;   // kLaunchSlots longest-first counting-sort scratches [hist | cursors]
+    std::array<bool, kLaunchSlots> hist_dirty{};  // histogram not known to be zero (fresh, failed launch)
     uint8_t* d_dummy = nullptr;   // a readable residue byte for batches with no residues
     LaunchRing kernels, orders;   // launch slots of the MSV kernel and of the order sort
     hipStream_t stream = nullptr;
@@ -243,6 +245,8 @@ struct msv_profile {
         uint64_t* h_off = nullptr;  // pinned rebased offsets
         size_t h_cap = 0;
         uint32_t* h_err = nullptr;  // pinned copy of the slot's error word
+        const float* direct = nullptr;  // page-locked destination written by the kernel (errors: scan)
+        uint64_t n = 0;
         hipEvent_t copied = nullptr, done = nullptr;
         uint64_t ticket = 0;
         bool pending = false;
@@ -266,6 +270,41 @@ struct msv_profile {
 // until the profile is destroyed or the binding ends (msv_profile_bind_stream flushes first).
 static bool lazy_stream(const msv_profile* p, hipStream_t st) {
     return st == p->stream || st == p->stream2 || (p->bound && st == p->bound);
+}
+
+// Device address of a page-locked host destination the kernels can write directly (nullptr for
+// pageable memory).  Host paths then need no score D2H: the kernels' stores cross PCIe as they are
+// made (a few MB of posted writes spread over the launch), and the end-of-kernel system-scope
+// release makes them visible before the completion the host waits on.  (A staged D2H of the scores
+// was dispatched as a blit KERNEL when queued behind the next call's launch, and starved there: the
+// persistent MSV grid holds every CU -- profiles/r02_host_pipeline_timeline.txt.)
+static float* mapped_host(float* host) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, host) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory is not an error here
+        return nullptr;
+    }
+    if (at.type != hipMemoryTypeHost) return nullptr;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<float*>(d);
+}
+
+// Errors of a batch whose scores went straight to host memory: a bad residue leaves +inf, a
+// too-long sequence NaN (msv_kernel.hip); valid scores are finite or -inf.
+static msv_status scan_scores(const float* scores, uint64_t n) {
+    bool inf = false, nan = false;
+    for (uint64_t i = 0; i < n; ++i) {
+        const float x = scores[i];
+        inf |= x == std::numeric_limits<float>::infinity();
+        nan |= x != x;
+    }
+    if (inf) return MSV_ERR_BAD_RESIDUE;
+    if (nan) return MSV_ERR_SEQUENCE_TOO_LONG;
+    return MSV_OK;
 }
 
 // Lays the MSV table out for variant v and uploads it:
@@ -733,11 +772,18 @@ msv_status msv_order_longest_first(msv_profile* p, const uint64_t* d_offsets, ui
     DeviceGuard g(p->device);
     if (!g.ok) return MSV_ERR_NO_DEVICE;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p->stream;
-    if (!p->d_hist)
-        MSV_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_hist), kLaunchSlots * kOrderBins * sizeof(uint32_t)));
+    if (!p->d_hist) {
+        MSV_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_hist), kLaunchSlots * 2 * kOrderBins * sizeof(uint32_t)));
+        p->hist_dirty.fill(true);
+    }
     int k = 0;
     MSV_HIP(p->orders.acquire(st, &k));
-    MSV_HIP(msvk::launch_order(d_offsets, n, p->d_hist + static_cast<size_t>(k) * kOrderBins, kOrderBins, d_order, st));
+    // [histogram | cursors] per slot; the sort leaves its histogram zeroed for the slot's next use
+    uint32_t* scratch = p->d_hist + static_cast<size_t>(k) * 2 * kOrderBins;
+    if (p->hist_dirty[k]) MSV_HIP(hipMemsetAsync(scratch, 0, kOrderBins * sizeof(uint32_t), st));
+    p->hist_dirty[k] = true;
+    MSV_HIP(msvk::launch_order(d_offsets, n, scratch, kOrderBins, d_order, st));
+    p->hist_dirty[k] = false;
     MSV_HIP(p->orders.release(k, st, lazy_stream(p, st)));
     return MSV_OK;
 }
@@ -776,7 +822,10 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     const size_t P = cut.size() - 1;
     MSV_HIP(ensure(p->d_res, p->d_res_cap, std::max<uint64_t>(total, 1)));
     MSV_HIP(ensure(p->d_off, p->d_off_cap, n + P));
-    MSV_HIP(ensure(p->d_scores, p->d_scores_cap, n));
+    // a page-locked destination is written by the kernels themselves (no D2H of the scores)
+    float* const direct = mapped_host(scores);
+    if (!direct) MSV_HIP(ensure(p->d_scores, p->d_scores_cap, n));
+    float* const dsc = direct ? direct : p->d_scores;
     MSV_HIP(ensure(p->d_order, p->d_order_cap, n));
     if (p->h_off_cap < n + P + 8) {  // pinned, so the offsets H2D is a true async DMA (+ the error word)
         if (p->h_off) (void)hipHostFree(p->h_off);
@@ -848,14 +897,14 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         hipStream_t c = cs[(P - 1 - k) & 1];
         if (pipe) MSV_HIP(hipStreamWaitEvent(c, p->events[2 + k], 0));
         s = launch_batch(p, bytes ? p->d_res + lo : p->d_dummy, std::max<uint64_t>(bytes, 1), p->d_off + cut[k] + k,
-                         cut[k + 1] - cut[k], p->d_order + cut[k], p->d_scores + cut[k], c, !pipe);
+                         cut[k + 1] - cut[k], p->d_order + cut[k], dsc + cut[k], c, !pipe);
         if (s != MSV_OK) return s;
     }
     if (pipe) {  // join the second compute stream (done before the last piece) back into the caller's
         MSV_HIP(hipEventRecord(p->events[P + 3], cs[1]));
         MSV_HIP(hipStreamWaitEvent(st, p->events[P + 3], 0));
     }
-    MSV_HIP(hipMemcpyAsync(scores, p->d_scores, n * sizeof(float), hipMemcpyDeviceToHost, st));
+    if (!direct) MSV_HIP(hipMemcpyAsync(scores, p->d_scores, n * sizeof(float), hipMemcpyDeviceToHost, st));
     MSV_HIP(hipMemcpyAsync(h_err, p->d_words + kErrWord, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     MSV_HIP(hipStreamSynchronize(st));  // also: the pinned h_off is rewritten by the next call
     drain.armed = false;
@@ -888,7 +937,8 @@ msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const 
     if (!a.h_err) MSV_HIP(hipHostMalloc(reinterpret_cast<void**>(&a.h_err), 64, hipHostMallocDefault));
     MSV_HIP(ensure(a.d_res, a.res_cap, std::max<uint64_t>(total, 1)));
     MSV_HIP(ensure(a.d_off, a.off_cap, n + 1));
-    MSV_HIP(ensure(a.d_sc, a.sc_cap, std::max<uint64_t>(n, 1)));
+    float* const direct = n ? mapped_host(scores) : nullptr;
+    if (!direct) MSV_HIP(ensure(a.d_sc, a.sc_cap, std::max<uint64_t>(n, 1)));
     MSV_HIP(ensure(a.d_ord, a.ord_cap, std::max<uint64_t>(n, 1)));
     if (a.h_cap < n + 1) {
         if (a.h_off) (void)hipHostFree(a.h_off);
@@ -901,7 +951,10 @@ msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const 
     for (uint64_t i = 0; i <= n; ++i) a.h_off[i] = n ? offsets[i] - base : 0;
     const int slot = static_cast<int>(&a - p->async);
     uint32_t* d_err = p->d_words + kErrWord + 1 + slot;
-    hipStream_t cp = p->copy_stream, cs = p->stream;
+    // Consecutive calls alternate over two compute streams, so a call's kernel fills the CUs that the
+    // previous call's drain tail frees instead of starting after the whole previous kernel.
+    if ((slot & 1) && !p->stream2) MSV_HIP(hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking));
+    hipStream_t cp = p->copy_stream, cs = (slot & 1) ? p->stream2 : p->stream;
     // copy stream: this call's inputs (they overlap the previous call's kernel on the compute stream)
     MSV_HIP(hipMemcpyAsync(a.d_off, a.h_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, cp));
     if (total) MSV_HIP(hipMemcpyAsync(a.d_res, residues + base, total, hipMemcpyHostToDevice, cp));
@@ -914,14 +967,18 @@ msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const 
     // compute stream: kernel, scores and the slot's error word back to the host
     MSV_HIP(hipStreamWaitEvent(cs, a.copied, 0));
     if (n) {
-        s = launch_batch(p, total ? a.d_res : p->d_dummy, std::max<uint64_t>(total, 1), a.d_off, n, a.d_ord, a.d_sc,
-                         cs, true, d_err);
+        s = launch_batch(p, total ? a.d_res : p->d_dummy, std::max<uint64_t>(total, 1), a.d_off, n, a.d_ord,
+                         direct ? direct : a.d_sc, cs, true, d_err);
         if (s != MSV_OK) return s;
-        MSV_HIP(hipMemcpyAsync(scores, a.d_sc, n * sizeof(float), hipMemcpyDeviceToHost, cs));
+        if (!direct) MSV_HIP(hipMemcpyAsync(scores, a.d_sc, n * sizeof(float), hipMemcpyDeviceToHost, cs));
     }
-    MSV_HIP(hipMemcpyAsync(a.h_err, d_err, sizeof(uint32_t), hipMemcpyDeviceToHost, cs));
-    MSV_HIP(hipMemsetAsync(d_err, 0, sizeof(uint32_t), cs));
+    if (!direct) {  // (direct: errors are read from the scores; nothing else follows the kernel)
+        MSV_HIP(hipMemcpyAsync(a.h_err, d_err, sizeof(uint32_t), hipMemcpyDeviceToHost, cs));
+        MSV_HIP(hipMemsetAsync(d_err, 0, sizeof(uint32_t), cs));
+    }
     MSV_HIP(hipEventRecord(a.done, cs));
+    a.direct = direct ? scores : nullptr;
+    a.n = n;
     a.ticket = p->next_ticket++;
     a.pending = true;
     *ticket = a.ticket;
@@ -936,6 +993,15 @@ msv_status msv_profile_wait(msv_profile* p, uint64_t ticket) {
         if (!g.ok) return MSV_ERR_NO_DEVICE;
         MSV_HIP(hipEventSynchronize(a.done));
         a.pending = false;
+        if (a.direct) {
+            const msv_status e = scan_scores(a.direct, a.n);
+            if (e != MSV_OK) {  // rare: clear the bits the kernel latched in the slot's error word
+                const int slot = static_cast<int>(&a - p->async);
+                MSV_HIP(hipMemsetAsync(p->d_words + kErrWord + 1 + slot, 0, sizeof(uint32_t), p->stream));
+                MSV_HIP(hipStreamSynchronize(p->stream));
+            }
+            return e;
+        }
         const uint32_t err = *a.h_err;
         if (err & msvk::kErrBadResidue) return MSV_ERR_BAD_RESIDUE;
         if (err & msvk::kErrTooLong) return MSV_ERR_SEQUENCE_TOO_LONG;

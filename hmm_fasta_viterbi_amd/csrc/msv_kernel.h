@@ -49,6 +49,8 @@ hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, h
 hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t n, float mu, float lambda,
                           double* pvalues, hipStream_t stream);
 
+// scratch_hist: 2 * nbins words [histogram | cursors]; the histogram must be zero on entry and is
+// zero again when the sort completes (zero it once when fresh, or after a failed launch).
 hipError_t launch_order(const uint64_t* offsets, uint64_t n, uint32_t* scratch_hist, uint32_t nbins, uint32_t* order,
                         hipStream_t stream);
 

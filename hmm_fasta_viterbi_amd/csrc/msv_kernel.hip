@@ -743,7 +743,9 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
 // Longest-first dequeue order: a device counting sort on sequence length (lengths >= nbins-1 share
 // the first bin).  Three small launches, histograms privatised in LDS so global atomics are one
 // per (block, non-empty bin):  count -> scan -> place.  Order inside a bin is arbitrary (it never
-// changes a score: every score is written to its own sequence's slot).
+// changes a score: every score is written to its own sequence's slot).  The scratch is [hist |
+// cursor]: the scan writes the cursors and zeroes the histogram for the next sort, so no memset
+// launch precedes a sort (the caller zeroes a fresh or failed scratch once).
 // ------------------------------------------------------------------------------------------------
 constexpr int kOrderThreads = 1024;
 
@@ -765,8 +767,9 @@ __global__ __launch_bounds__(kOrderThreads) void order_count_kernel(const uint64
         if (lh[i]) atomicAdd(&hist[i], lh[i]);
 }
 
-// Exclusive scan of hist[nbins] in place (one block; nbins <= 4 * kOrderThreads).
-__global__ __launch_bounds__(kOrderThreads) void order_scan_kernel(uint32_t* __restrict__ hist, uint32_t nbins) {
+// Exclusive scan of hist[nbins] into cursor[nbins], hist zeroed (one block; nbins <= 4 * kOrderThreads).
+__global__ __launch_bounds__(kOrderThreads) void order_scan_kernel(uint32_t* __restrict__ hist,
+                                                                   uint32_t* __restrict__ cursor, uint32_t nbins) {
     __shared__ uint32_t part[kOrderThreads];
     const uint32_t t = threadIdx.x;
     uint32_t v[4], sum = 0;
@@ -774,6 +777,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_scan_kernel(uint32_t* __r
     for (int q = 0; q < 4; ++q) {
         const uint32_t i = 4 * t + q;
         v[q] = i < nbins ? hist[i] : 0u;
+        if (i < nbins) hist[i] = 0u;
         sum += v[q];
     }
     part[t] = sum;
@@ -788,7 +792,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_scan_kernel(uint32_t* __r
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint32_t i = 4 * t + q;
-        if (i < nbins) hist[i] = run;
+        if (i < nbins) cursor[i] = run;
         run += v[q];
     }
 }
@@ -933,16 +937,15 @@ hipError_t launch_order(const uint64_t* offsets, uint64_t n, uint32_t* scratch_h
                            static_cast<uint32_t>(n), nbins, order);
         return hipGetLastError();
     }
-    hipError_t e = hipMemsetAsync(scratch_hist, 0, nbins * sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
     const uint64_t blocks = std::min<uint64_t>(256, (n + 511) / 512);
     const uint64_t chunk = (n + blocks - 1) / blocks;
     const size_t lds = nbins * sizeof(uint32_t);
     hipLaunchKernelGGL(order_count_kernel, dim3(blocks), dim3(kOrderThreads), lds, stream, offsets, n, chunk,
                        scratch_hist, nbins);
-    hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(kOrderThreads), 0, stream, scratch_hist, nbins);
+    hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(kOrderThreads), 0, stream, scratch_hist,
+                       scratch_hist + nbins, nbins);
     hipLaunchKernelGGL(order_place_kernel, dim3(blocks), dim3(kOrderThreads), lds, stream, offsets, n, chunk,
-                       scratch_hist, nbins, order);
+                       scratch_hist + nbins, nbins, order);
     return hipGetLastError();
 }
 

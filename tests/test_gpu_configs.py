@@ -232,6 +232,50 @@ def test_async_stream_of_batches():
     e.close()
 
 
+def test_pinned_destinations_written_by_kernel():
+    """Page-locked score destinations are written by the kernels themselves (no D2H): the one-call
+    pipeline and the async stream of batches return the staged paths' scores bitwise; a bad residue
+    in a direct async call is found from its +inf score, reported by that call's wait only, and
+    leaves no latched bit behind for the next (staged) call on the same slot."""
+    import torch
+    from hmm_fasta_viterbi_amd._native import MSVError
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("1400.hmm")))
+    batches = [random_batch(500 + k, n, 0, 700) for k, n in enumerate((40_000, 3, 15_000, 25_000))]
+    want = [e.score_batch(codes=c, offsets=o) for c, o in batches]
+    pin = lambda n: torch.full((n,), float("nan"), dtype=torch.float32).pin_memory().numpy()
+    big_c, big_o = random_batch(510, 30_000, 100, 400)  # >= 4 Mi residues: the piece pipeline
+    assert int(big_o[-1]) >= 4 << 20
+    big_want = e.score_batch(codes=big_c, offsets=big_o)
+    got = e.score_batch(codes=big_c, offsets=big_o, out=pin(len(big_o) - 1))
+    assert np.array_equal(bits(got), bits(big_want))
+    outs = [pin(len(o) - 1) for _, o in batches]
+    tickets, got = [], []
+    for k, ((c, o), out) in enumerate(zip(batches, outs)):
+        tickets.append(e.score_batch_async(c, o, out=out))
+        if k >= 1:
+            got.append(e.wait(tickets[k - 1]))
+    got.append(e.wait(tickets[-1]))
+    for k, (g, w) in enumerate(zip(got, want)):
+        assert np.array_equal(bits(g), bits(w)), k
+    bad_c = batches[0][0].copy()
+    bad_c[int(batches[0][1][7]) + 2] = 31
+    for slot_pair in range(2):  # both staging slots take a direct bad call, then a staged good one
+        if slot_pair:  # shift the slot parity by one call
+            assert np.array_equal(bits(e.wait(e.score_batch_async(*batches[1]))), bits(want[1]))
+        t_bad = e.score_batch_async(bad_c, batches[0][1], out=pin(len(batches[0][1]) - 1))
+        t_ok = e.score_batch_async(batches[2][0], batches[2][1], out=pin(len(batches[2][1]) - 1))
+        with pytest.raises(IndexError):
+            e.wait(t_bad)
+        assert np.array_equal(bits(e.wait(t_ok)), bits(want[2])), slot_pair
+        t1 = e.score_batch_async(batches[3][0], batches[3][1])  # pageable: staged D2H + error word
+        t2 = e.score_batch_async(batches[2][0], batches[2][1])
+        assert np.array_equal(bits(e.wait(t1)), bits(want[3]))
+        assert np.array_equal(bits(e.wait(t2)), bits(want[2]))
+    with pytest.raises(MSVError):
+        e.wait(t2)
+    e.close()
+
+
 def test_rccl_multi_device_context():
     """msv_multi_*: ncclCommInitAll over the given devices, shards scored per device, scores gathered
     into device 0 by ONE grouped ncclSend/ncclRecv (rank 0 through a self send/recv), one D2H.  On a
