@@ -251,10 +251,17 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     const bool sameEJ = __float_as_uint(tEC) == __float_as_uint(tEJ);  // wave-uniform (SGPR)
 
     uint32_t rows_done = 0;  // rows issued by this wave (diagnostics)
-    // Work distribution: a group takes its first sequence when it starts; the index of its next
-    // sequence is fetched when the current one is half done (so the atomic's latency hides behind
-    // half a sequence, and a batch smaller than twice the number of groups is still spread one
-    // sequence per group instead of two per early group).
+    // Work distribution: a group's first sequence is its group number; the index of its next sequence
+    // is fetched while the current one runs.  Long rows (S >= 64) fetch it 8 + 256/S rows before the
+    // end -- enough to hide the atomic's round trip, late enough that the last indices go to the
+    // groups actually about to finish rather than to every group half-way through its sequence:
+    // cfg5 25.50 -> 25.03 ms, cfg3 neutral.  Short rows fetch half-way: their sequences end ~100 per
+    // us, and at that rate the one counter's atomics queue for more than 17 rows of 28 states
+    // (400.hmm x 100k: 1.034 vs 1.004 ms late; profiles/r02_ab_fetch_ahead.jsonl).
+#ifndef MSV_FETCH_AHEAD
+#define MSV_FETCH_AHEAD (S >= 64 ? 8 + 256 / S : 0xFFFFFFFFu)
+#endif
+    constexpr uint32_t kFetchAhead = MSV_FETCH_AHEAD;
     constexpr uint32_t kNone = 0xFFFFFFFFu;
     const uint32_t n_groups = gridDim.x * (WAVES * 64 / G);  // statically assigned first indices
     // the group's first sequence: its own group number (the first stream's begin consumes it)
@@ -301,8 +308,9 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         st.endpos = run ? static_cast<uint32_t>(o1 - 1) : 0u;
         // a junk stream ends after its one row; a retired one never (pos cannot reach 2^32 - 1)
         st.endp = retire ? 0xFFFFFFFFu : (run ? static_cast<uint32_t>(o1) : 1u);
-        // the next index is fetched after L - L/2 rows (equal to endp when L == 1: begin fetches it)
-        st.ev = run ? static_cast<uint32_t>(o1 - (L >> 1)) : st.endp;
+        // the next index is fetched kFetchAhead rows before the end (half-way for shorter sequences;
+        // equal to endp when L == 1: begin fetches it)
+        st.ev = run ? static_cast<uint32_t>(o1 - min(L >> 1, static_cast<uint64_t>(kFetchAhead))) : st.endp;
 #pragma unroll
         for (int k = 0; k < S; ++k) st.M[k] = NINF;
         st.J = NINF;
