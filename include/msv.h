@@ -171,18 +171,22 @@ msv_status msv_profile_reserve_length(msv_profile* profile, uint64_t max_length)
  * MSV_HMM::run_on_sequence (MSV_HMM.cpp:74-113); an empty sequence scores -inf.
  * stream may be NULL (the library's own stream).  Batches of >= 4 Mi residues run as a copy/compute
  * pipeline (H2D of later pieces under the kernels of earlier ones); residues in pinned host memory
- * (hipHostMalloc, torch pin_memory) copy at full PCIe rate without runtime staging. */
+ * (hipHostMalloc, torch pin_memory) copy at full PCIe rate without runtime staging.  Pinned `scores`
+ * are written by the kernels themselves through their device alias (no D2H copy). */
 msv_status msv_score_batch(msv_profile* profile, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
                            float* scores, void* stream);
 
 /* Asynchronous host-buffer scoring for a STREAM of batches (serving): enqueues the H2D of the
- * inputs on the profile's copy stream and the order, kernel and score D2H on its compute stream, and
+ * inputs on the profile's copy stream and the order, kernel and score D2H on one of its two compute
+ * streams (consecutive calls alternate, so a call's kernel fills the previous one's drain tail), and
  * returns at once with a ticket; msv_profile_wait(ticket) blocks until that call's scores are in
  * `scores` and returns its kernel-latched errors.  Two staging sets, so the copy of call k+1 runs
  * under the kernel of call k; at most 2 calls may be outstanding (a third returns
  * MSV_ERR_INVALID_ARGUMENT until the oldest is waited for).  The caller keeps residues/offsets
  * unchanged and does not read scores until the wait; pinned (page-locked) host buffers make the
- * copies truly asynchronous.  One launch per call: residues < 2^32 - 2^20 bytes. */
+ * copies truly asynchronous, and pinned `scores` are written by the kernel directly (no D2H; that
+ * call's errors are then read from its scores: +inf = bad residue, NaN = too long).  One launch per
+ * call: residues < 2^32 - 2^20 bytes. */
 msv_status msv_score_batch_async(msv_profile* profile, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
                                  float* scores, uint64_t* ticket);
 msv_status msv_profile_wait(msv_profile* profile, uint64_t ticket);
