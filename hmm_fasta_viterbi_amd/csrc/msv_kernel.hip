@@ -220,8 +220,13 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // the waits the compiler places at the loop header or after a rare path (which merge every load
     // in flight: with per-row slots the header waited for the load of the row before, once per RPF
     // rows -- the bound of cfg2's 100.hmm rows) find it landed.  16x fewer VMEM instructions.
-    constexpr bool BLK = ROT && G >= 16 && !SPLIT;
-    constexpr int NPH = BLK ? 16 : St::RPF;  // phases of the unrolled row loop
+#ifndef MSV_BLK_LARGE
+#define MSV_BLK_LARGE 0
+#endif
+    // rows per block: 16 for short rows; long rows (one residue of prefetch) optionally 8 (experiment)
+    constexpr int BLKN = St::RPF > 1 ? 16 : MSV_BLK_LARGE;
+    constexpr bool BLK = !BIG && D == 1 && G >= 16 && !SPLIT && BLKN > 0;
+    constexpr int NPH = BLK ? BLKN : St::RPF;  // phases of the unrolled row loop
     // Cross-row emission prefetch: when the ring holds a whole row (small profiles), the NEXT row's
     // chunks are requested right after this row's last cell update, so the LDS latency hides behind
     // the E butterfly and the specials instead of stalling the start of every row.
@@ -268,7 +273,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     uint32_t pending = (blockIdx.x * WAVES + (threadIdx.x >> 6)) * (64 / G) + static_cast<uint32_t>(lane / G);
 
     using Ph0 = std::integral_constant<int, 0>;
-    const uint32_t blk_lane = static_cast<uint32_t>(gl & 15);  // BLK: the lane's row within a block
+    const uint32_t blk_lane = static_cast<uint32_t>(gl & (BLKN > 0 ? BLKN - 1 : 0));  // BLK: the lane's row in a block
 
     // Start the next non-empty sequence in a stream (or retire the stream); `ph` is the phase of the
     // row that will run next (its residue goes to slot r[ph]).
@@ -324,7 +329,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             // pos + 16 + b - PH.  PH = 0: the phase-0 row first moves nxt into cur, so both hold the
             // first block.  (Lanes below PH are never read; max() keeps their index >= pos.)
             const uint32_t ic = max(st.pos + blk_lane, st.pos + PH) - PH;
-            const uint32_t in = PH == 0 ? ic : st.pos + blk_lane + (16 - PH);
+            const uint32_t in = PH == 0 ? ic : st.pos + blk_lane + (BLKN - PH);
             st.cur = min(static_cast<uint32_t>(res[min(ic, st.endpos)]), static_cast<uint32_t>(kPoisonRow));
             st.nxt = res[min(in, st.endpos)];
         } else {
@@ -337,10 +342,10 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     auto resid = [&](St& st, auto pp) __attribute__((always_inline)) -> uint32_t {
         constexpr int P = decltype(pp)::value;
         if constexpr (BLK) {
-            if constexpr (P < 16) {
+            if constexpr (P < BLKN) {
                 return row_bcast_lane<P>(st.cur);
             } else {
-                return min(row_bcast_lane<P - 16>(static_cast<uint32_t>(st.nxt)), static_cast<uint32_t>(kPoisonRow));
+                return min(row_bcast_lane<P - BLKN>(static_cast<uint32_t>(st.nxt)), static_cast<uint32_t>(kPoisonRow));
             }
         } else {
             return st.r[P % St::RPF];
@@ -610,7 +615,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         if constexpr (BLK && PH == 0) {
             // a new 16-row block: the one loaded 16 rows ago becomes current, the next is requested
             s0.cur = min(static_cast<uint32_t>(s0.nxt), static_cast<uint32_t>(kPoisonRow));
-            s0.nxt = res[min(s0.pos + 16 + blk_lane, s0.endpos)];
+            s0.nxt = res[min(s0.pos + BLKN + blk_lane, s0.endpos)];
         }
         if constexpr (XROW2) {
             RowCtx<PF>& rc = (PH & 1) ? xr1 : xr;
@@ -656,7 +661,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     };
 
     while (live) {
-        if constexpr (ROT) {
+        if constexpr (ROT || BLK) {
             // NPH rows per iteration (residue slots, or the 16 rows of a BLK block); stops after any row that retires the wave
             [&]<int... I>(std::integer_sequence<int, I...>) {
                 (void)(step(std::integral_constant<int, I>{}) && ...);
