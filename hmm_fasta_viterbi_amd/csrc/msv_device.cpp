@@ -231,6 +231,7 @@ struct msv_profile {
     size_t h_off_cap = 0;
     uint32_t pipe_first_den = 4, pipe_growth = 2;  // piece sizes: total / first_den, then x growth
     uint32_t pipe_streams = 2;                      // compute streams the pieces alternate over
+    bool zero_copy = true;  // page-locked residues read in place (msv_debug_set_zero_copy turns it off)
     // msv_score_batch_async: kAsyncSlots staging sets, so the H2D of one call runs under the kernel
     // of the call before it
     struct AsyncSlot {
@@ -278,19 +279,22 @@ static bool lazy_stream(const msv_profile* p, hipStream_t st) {
 // release makes them visible before the completion the host waits on.  (A staged D2H of the scores
 // was dispatched as a blit KERNEL when queued behind the next call's launch, and starved there: the
 // persistent MSV grid holds every CU -- profiles/r02_host_pipeline_timeline.txt.)
-static float* mapped_host(float* host) {
+// (The same alias lets a kernel READ page-locked residues in place: see msv_score_batch.)
+template <typename T>
+static T* mapped_host(T* host) {
     hipPointerAttribute_t at{};
-    if (hipPointerGetAttributes(&at, host) != hipSuccess) {
+    void* h = const_cast<void*>(static_cast<const void*>(host));
+    if (hipPointerGetAttributes(&at, h) != hipSuccess) {
         (void)hipGetLastError();  // pageable memory is not an error here
         return nullptr;
     }
     if (at.type != hipMemoryTypeHost) return nullptr;
     void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess) {
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
-    return static_cast<float*>(d);
+    return static_cast<T*>(d);
 }
 
 // Errors of a batch whose scores went straight to host memory: a bad residue leaves +inf, a
@@ -644,6 +648,14 @@ msv_status msv_debug_set_pipeline(msv_profile* p, uint32_t first_den, uint32_t g
     return MSV_OK;
 }
 
+// Diagnostics (not in msv.h): msv_score_batch reads page-locked residues in place (1, default) or
+// copies them through the piece pipeline like pageable ones (0).
+msv_status msv_debug_set_zero_copy(msv_profile* p, int on) {
+    if (!p) return MSV_ERR_INVALID_ARGUMENT;
+    p->zero_copy = on != 0;
+    return MSV_OK;
+}
+
 int msv_debug_grid_waves(const msv_profile* p) {
     if (!p) return 0;
     const int lat = p->lat.v ? p->lat.blocks * p->lat.v->waves : 0;
@@ -818,9 +830,15 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     // launch has its own dequeue counter slot).  Scores and the error word come back once at the end
     // (pageable destinations would make per-piece D2H copies block the host thread that enqueues the
     // pipeline), followed by ONE synchronisation.
-    const std::vector<uint64_t> cut = plan_pieces(offsets, n, total, p->pipe_first_den, p->pipe_growth);
+    // Page-locked residues are not copied at all: the kernel reads them in place over PCIe through their
+    // device alias (zero-copy; L2 keeps each 128-B line for the rows that follow).  cfg3: kernel 2.98 vs
+    // 2.87 ms from HBM -- 0.96 of the resident rate with no copy, against ~0.85 for the copy pipeline
+    // below, whose first piece's copy and extra drain tail it saves (profiles/r02_zero_copy_probe.jsonl).
+    // One launch per < 2^32-byte piece; no copy stream, no second compute stream.
+    const uint8_t* const zres = (total && p->zero_copy) ? mapped_host(residues) : nullptr;
+    const std::vector<uint64_t> cut = plan_pieces(offsets, n, total, zres ? 0 : p->pipe_first_den, p->pipe_growth);
     const size_t P = cut.size() - 1;
-    MSV_HIP(ensure(p->d_res, p->d_res_cap, std::max<uint64_t>(total, 1)));
+    if (!zres) MSV_HIP(ensure(p->d_res, p->d_res_cap, std::max<uint64_t>(total, 1)));
     MSV_HIP(ensure(p->d_off, p->d_off_cap, n + P));
     // a page-locked destination is written by the kernels themselves (no D2H of the scores)
     float* const direct = mapped_host(scores);
@@ -835,7 +853,7 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         p->h_off_cap = n + P + 8;
     }
     uint32_t* h_err = reinterpret_cast<uint32_t*>(p->h_off + n + P);
-    const bool pipe = P > 1;
+    const bool pipe = P > 1 && !zres;
     hipStream_t cs[2] = {st, st}, cp = st;
     // On an early error return, copies reading the pinned h_off (rewritten by the next call) and
     // kernels writing the staging buffers may still be queued: drain every stream used first.
@@ -869,7 +887,8 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     const uint64_t base0 = offsets[0];
     for (size_t k = 0; k < P; ++k) {
         const uint64_t lo = offsets[cut[k]] - base0, bytes = offsets[cut[k + 1]] - offsets[cut[k]];
-        if (bytes) MSV_HIP(hipMemcpyAsync(p->d_res + lo, residues + base0 + lo, bytes, hipMemcpyHostToDevice, cp));
+        if (bytes && !zres)
+            MSV_HIP(hipMemcpyAsync(p->d_res + lo, residues + base0 + lo, bytes, hipMemcpyHostToDevice, cp));
         if (pipe) MSV_HIP(hipEventRecord(p->events[2 + k], cp));  // piece k's residues landed
     }
     // 2. meanwhile every piece's offsets (rebased on the piece's first residue, at h_off[cut[k] + k ..])
@@ -896,7 +915,8 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         const uint64_t lo = offsets[cut[k]] - base0, bytes = offsets[cut[k + 1]] - offsets[cut[k]];
         hipStream_t c = cs[(P - 1 - k) & 1];
         if (pipe) MSV_HIP(hipStreamWaitEvent(c, p->events[2 + k], 0));
-        s = launch_batch(p, bytes ? p->d_res + lo : p->d_dummy, std::max<uint64_t>(bytes, 1), p->d_off + cut[k] + k,
+        const uint8_t* src = zres ? zres + base0 + lo : p->d_res + lo;
+        s = launch_batch(p, bytes ? src : p->d_dummy, std::max<uint64_t>(bytes, 1), p->d_off + cut[k] + k,
                          cut[k + 1] - cut[k], p->d_order + cut[k], dsc + cut[k], c, !pipe);
         if (s != MSV_OK) return s;
     }

@@ -276,6 +276,43 @@ def test_pinned_destinations_written_by_kernel():
     e.close()
 
 
+def test_zero_copy_pinned_residues():
+    """Page-locked residues are read by the kernel in place (no H2D): bitwise equal to the copy
+    pipeline (zero-copy switched off) and to a device launch -- for a > 4 Mi-residue batch (one launch
+    instead of pieces), an offsets array not starting at 0, a view starting inside the pinned
+    allocation, a pinned buffer rewritten between calls, and a bad residue (raises)."""
+    import ctypes as C
+    import torch
+    from hmm_fasta_viterbi_amd import _native
+    L = _native.lib()
+    L.msv_debug_set_zero_copy.argtypes = [C.c_void_p, C.c_int]
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("1400.hmm")))
+    codes, offsets = random_batch(520, 30_000, 0, 600)
+    assert int(offsets[-1]) >= 4 << 20
+    want = device_scores(e, codes, offsets)
+    pinned = torch.from_numpy(codes).pin_memory().numpy()
+    got = e.score_batch(codes=pinned, offsets=offsets)
+    assert np.array_equal(bits(got), bits(want))
+    assert L.msv_debug_set_zero_copy(e._p, 0) == 0  # the copy pipeline on the same pinned source
+    assert np.array_equal(bits(e.score_batch(codes=pinned, offsets=offsets)), bits(want))
+    assert L.msv_debug_set_zero_copy(e._p, 1) == 0
+    sub = e.score_batch(codes=pinned, offsets=offsets[7000:])  # offsets[0] != 0
+    assert np.array_equal(bits(sub), bits(want[7000:]))
+    base = int(offsets[123])  # a view whose first byte is inside the pinned allocation
+    view = e.score_batch(codes=pinned[base:], offsets=(offsets[123:] - base).astype(np.uint64))
+    assert np.array_equal(bits(view), bits(want[123:]))
+    c2, o2 = random_batch(521, 30_000, 0, 600)  # rewrite the same pinned buffer
+    m = min(len(c2), len(pinned))
+    keep = int(np.searchsorted(o2, m, side="right")) - 1
+    pinned[:int(o2[keep])] = c2[:int(o2[keep])]
+    want2 = e.score_batch(codes=c2, offsets=o2[:keep + 1])  # pageable: copied
+    assert np.array_equal(bits(e.score_batch(codes=pinned, offsets=o2[:keep + 1])), bits(want2))
+    pinned[int(o2[5]) + 3] = 22
+    with pytest.raises(IndexError):
+        e.score_batch(codes=pinned, offsets=o2[:keep + 1])
+    e.close()
+
+
 def test_rccl_multi_device_context():
     """msv_multi_*: ncclCommInitAll over the given devices, shards scored per device, scores gathered
     into device 0 by ONE grouped ncclSend/ncclRecv (rank 0 through a self send/recv), one D2H.  On a
