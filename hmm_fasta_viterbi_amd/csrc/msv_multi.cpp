@@ -3,7 +3,8 @@
 //
 // The reference has no multi-device path.  Sequences are independent, so the batch is cut
 // into contiguous shards of ~equal residue count (msv_shard_bounds); one host thread per device
-// uploads its shard and enqueues the longest-first order and ONE kernel launch on the device's stream;
+// uploads its shard (or, for page-locked residues, lets its kernel read them in place) and enqueues the
+// longest-first order and ONE kernel launch on the device's stream;
 // then a single RCCL group moves every shard's float scores into device 0's result buffer at the
 // shard's offset (exact counts, no padding; rank 0's own shard goes through a self send/recv, so the
 // exchange code runs even with one device), and one D2H returns them.  Only public msv.h entry points
@@ -89,6 +90,23 @@ struct DeviceGuard {
     }
 };
 
+// Device alias of page-locked host residues (nullptr for pageable memory): every rank's kernel then
+// reads its shard in place over its own PCIe link instead of a staged copy (as msv_score_batch does).
+const uint8_t* pinned_alias(const uint8_t* host) {
+    hipPointerAttribute_t at{};
+    void* h = const_cast<uint8_t*>(host);
+    if (!host || hipPointerGetAttributes(&at, h) != hipSuccess || at.type != hipMemoryTypeHost) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<const uint8_t*>(d);
+}
+
 // Upload shard [first, last) to rank r's device and enqueue its order + kernel launches (one per
 // < 4 GiB chunk) on the rank's stream.  Runs on the rank's own host thread.
 msv_status enqueue_shard(Rank& r, const uint8_t* residues, const uint64_t* offsets, uint64_t first, uint64_t last) {
@@ -96,22 +114,28 @@ msv_status enqueue_shard(Rank& r, const uint8_t* residues, const uint64_t* offse
     if (!g.ok) return MSV_ERR_NO_DEVICE;
     const uint64_t cn = last - first;
     MM_HIP(grow(r.d_sc, r.sc_cap, cn));
+    const uint8_t* const zres = pinned_alias(residues);
     uint64_t a = first;
     while (a < last) {  // chunks addressing < kChunkBytes residues each
         uint64_t b = a + 1;
         while (b < last && offsets[b + 1] - offsets[a] < kChunkBytes) ++b;
         if (offsets[b] - offsets[a] >= kChunkBytes) return MSV_ERR_SEQUENCE_TOO_LONG;
         const uint64_t n = b - a, base = offsets[a], bytes = offsets[b] - base;
-        MM_HIP(grow(r.d_res, r.res_cap, std::max<uint64_t>(bytes, 1)));
+        if (!zres) MM_HIP(grow(r.d_res, r.res_cap, std::max<uint64_t>(bytes, 1)));
         MM_HIP(grow(r.d_off, r.off_cap, n + 1));
         MM_HIP(grow(r.d_ord, r.ord_cap, n));
         r.h_off.resize(n + 1);
         for (uint64_t i = 0; i <= n; ++i) r.h_off[i] = offsets[a + i] - base;
         MM_HIP(hipMemcpyAsync(r.d_off, r.h_off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, r.stream));
-        if (bytes) MM_HIP(hipMemcpyAsync(r.d_res, residues + base, bytes, hipMemcpyHostToDevice, r.stream));
+        if (bytes && !zres) MM_HIP(hipMemcpyAsync(r.d_res, residues + base, bytes, hipMemcpyHostToDevice, r.stream));
         msv_status s = msv_order_longest_first(r.profile, r.d_off, n, r.d_ord, r.stream);
         if (s != MSV_OK) return s;
-        s = msv_score_batch_device(r.profile, r.d_res, std::max<uint64_t>(bytes, 1), r.d_off, n, r.d_ord,
+        const uint8_t* src = (zres && bytes) ? zres + base : (bytes ? r.d_res : nullptr);
+        if (!src) {  // an all-empty chunk still needs one readable byte
+            MM_HIP(grow(r.d_res, r.res_cap, 1));
+            src = r.d_res;
+        }
+        s = msv_score_batch_device(r.profile, src, std::max<uint64_t>(bytes, 1), r.d_off, n, r.d_ord,
                                    r.d_sc + (a - first), r.stream);
         if (s != MSV_OK) return s;
         // h_off (pageable) is rewritten by the next chunk: let this chunk's copy finish first

@@ -330,6 +330,11 @@ def test_rccl_multi_device_context():
     assert np.array_equal(bits(got), bits(want))
     small = multi.score_batch(codes=codes[:int(offsets[3])], offsets=offsets[:4])  # fewer sequences than ranks
     assert np.array_equal(bits(small), bits(want[:3]))
+    import torch
+    pinned = torch.from_numpy(codes).pin_memory().numpy()  # shards read in place by every rank's kernel
+    assert np.array_equal(bits(multi.score_batch(codes=pinned, offsets=offsets)), bits(want))
+    empty = multi.score_batch(codes=pinned[:0], offsets=np.zeros(5, np.uint64))  # all-empty, pinned source
+    assert np.all(empty == -np.inf)
     idx = sample_with_extremes(offsets, 64, 9)
     assert np.array_equal(bits(got[idx]), bits(OracleProfile("1400").score_batch(*subset(codes, offsets, idx),
                                                                                   threads=ORACLE_THREADS)))
