@@ -1048,7 +1048,14 @@ msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profil
         ~EventGuard() { (void)hipEventDestroy(e); }
     } fork_guard{fork};
     MSV_HIP(hipEventRecord(fork, cs));
-    for (uint32_t i = 0; i < n_profiles; ++i) {
+    // Largest models first: their launches are the longest, and with more streams than hardware queues
+    // (HIP's default is 4) the launches queued behind them are the short ones.
+    std::vector<uint32_t> launch_order(n_profiles);
+    for (uint32_t i = 0; i < n_profiles; ++i) launch_order[i] = i;
+    std::stable_sort(launch_order.begin(), launch_order.end(), [&](uint32_t x, uint32_t y) {
+        return profiles[x]->model_length > profiles[y]->model_length;
+    });
+    for (const uint32_t i : launch_order) {
         msv_profile* p = profiles[i];
         if (!p->done) MSV_HIP(hipEventCreateWithFlags(&p->done, hipEventDisableTiming));
         hipStream_t ps = p->stream == cs ? cs : p->stream;
@@ -1119,11 +1126,16 @@ msv_status msv_score_grid(msv_profile* const* profiles, uint32_t n_profiles, con
     if (s != MSV_OK) return s;
     MSV_HIP(hipMemcpyAsync(scores, b.sc, total * sizeof(float), hipMemcpyDeviceToHost, st));
     MSV_HIP(hipStreamSynchronize(st));  // pageable host buffers above
+    // This call's errors show in its scores (+inf: bad residue, NaN: too long), so the profiles' latched
+    // error words are read back only when there is one (a 4-byte read-back per profile is a blit kernel
+    // plus a synchronisation: 24 profiles cost 0.9 ms, more than the whole grid's kernels).
+    if (scan_scores(scores, total) == MSV_OK) return MSV_OK;
+    msv_status first = MSV_OK;  // read back and clear EVERY profile's latched bits, report the first
     for (uint32_t i = 0; i < n_profiles; ++i) {
         s = msv_profile_check(profiles[i], st);
-        if (s != MSV_OK) return s;
+        if (first == MSV_OK) first = s;
     }
-    return MSV_OK;
+    return first != MSV_OK ? first : scan_scores(scores, total);
 }
 
 // Host restatement of msvk::msv_pvalue_of (kept textually parallel; tests compare both).

@@ -287,6 +287,21 @@ def test_score_grid_random_fasta_and_seeded():
         assert np.array_equal(bits(grid[k]), bits(engine(prof).score_batch(codes=codes, offsets=offsets))), prof
 
 
+def test_score_grid_bad_residue_reported_then_cleared():
+    """A bad residue in a grid call raises (read from the call's +inf scores, then the profiles' latched
+    words are read back and cleared), and the next grid call on good input succeeds bitwise."""
+    codes, offsets = random_batch(33, 200, 1, 400)
+    sub = [engine(p) for p in ("200.hmm", "1400.hmm", "2405.hmm")]
+    want = msv.score_grid(sub, codes=codes, offsets=offsets)
+    bad = codes.copy()
+    bad[int(offsets[17]) + 1] = 200
+    with pytest.raises(IndexError):
+        msv.score_grid(sub, codes=bad, offsets=offsets)
+    assert np.array_equal(bits(msv.score_grid(sub, codes=codes, offsets=offsets)), bits(want))
+    for e in sub:
+        e.check()
+
+
 def test_score_grid_device_torch_stream():
     import torch
     codes, offsets = random_batch(32, 2000, 1, 700)

@@ -23,6 +23,10 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# score_grid forks one launch per profile onto the profiles' own streams; HIP's default of 4 hardware
+# queues runs at most 4 of the 24 small launches at once (as bench.py, raise it before HIP starts).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 PROFILES = sorted((f for f in os.listdir(os.path.join(ROOT, "data", "profile_HMMs")) if f.endswith(".hmm")),
                   key=lambda f: int(f.split(".")[0]))
 
