@@ -103,7 +103,9 @@ msv_status hip_status(hipError_t e) {
 // A split table (the lane's last S - SA states read from L2 every row) costs the B-table address and
 // loads per row and no class branch, so it also runs two sequences per wave (G = 32).
 double variant_cost(const msvk::Variant& v) {
-    const double big = !v.big ? 1.0 : (v.G == 64 ? 1.03 : 1.6);
+    // (G = 64 BIG: 1.15 -- 1901.hmm's 64 x 32 row-class plan measured 1.12 / 2.20 ms against 0.97 / 1.99 ms
+    // for the 64 x 34 split plan at 3 / 2048 sequences, profiles/r02_latency_plans.jsonl)
+    const double big = !v.big ? 1.0 : (v.G == 64 ? 1.15 : 1.6);
     // G = 64: + permlane32 step, scalar bookkeeping
     const double row = (v.G == 64 ? 36.0 : 26.0) + (v.sa ? 2.0 : 0.0);
     return (2.5 * v.S + row) * v.G * big * (v.pf == 2 ? 1.0 : 1.05) * (v.streams == 2 ? 1.15 : 1.0);
@@ -386,11 +388,13 @@ static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
     if (s != MSV_OK) return s;
     const msvk::Variant* lv = p->force ? nullptr : pick_latency_variant(p->model_length - 1);
     // Worth it only when the 64-lane row is much shorter than the main row (per-row issue cost,
-    // as variant_cost): 1400.hmm 246 vs 96 -> 0.25 vs 0.55 ms at 512 sequences, still ahead at 8192;
-    // 100.hmm 46 vs 46 -> slower at every size (tools/tune.py, profiles/r01_latency_plan.jsonl).
-    const double main_row = 2.5 * v->S + 26.0, lat_row = lv ? 2.5 * lv->S + 36.0 : 0.0;
+    // as variant_cost): 1400.hmm 246 vs 96 -> 0.23 vs 0.62 ms at 1024 sequences, 0.37 vs 0.64 at 8192,
+    // even at 16384; 1901.hmm 176 vs 123 -> 0.97 vs 1.29 ms at 3 sequences, 1.99 vs 2.89 at 2048;
+    // 100.hmm 46 vs 46 -> slower at every size (tools/tune.py, profiles/r01_latency_plan.jsonl,
+    // r02_latency_plans.jsonl).
+    const double main_row = 2.5 * v->S + 26.0, lat_row = lv ? 2.5 * lv->S + 36.0 + (lv->sa ? 2.0 : 0.0) : 0.0;
     const double ratio = lv ? main_row / lat_row : 0.0;
-    if (!lv || lv == v || ratio < 1.6) {
+    if (!lv || lv == v || ratio < 1.3) {
         if (p->lat.d_etab) {
             (void)hipDeviceSynchronize();
             (void)hipFree(p->lat.d_etab);
@@ -399,7 +403,7 @@ static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
         p->lat_max_n = 0;
         return MSV_OK;
     }
-    p->lat_max_n = static_cast<uint64_t>(std::min(8192.0, 4096.0 * ratio / 1.6));
+    p->lat_max_n = static_cast<uint64_t>(std::min(12288.0, 4096.0 * ratio));
     return install_plan(p, lv, p->lat);
 }
 

@@ -269,8 +269,23 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     constexpr uint32_t kFetchAhead = MSV_FETCH_AHEAD;
     constexpr uint32_t kNone = 0xFFFFFFFFu;
     const uint32_t n_groups = gridDim.x * (WAVES * 64 / G);  // statically assigned first indices
-    // the group's first sequence: its own group number (the first stream's begin consumes it)
-    uint32_t pending = (blockIdx.x * WAVES + (threadIdx.x >> 6)) * (64 / G) + static_cast<uint32_t>(lane / G);
+    // The group's first sequence (the first stream's begin consumes it).  With the longest-first order,
+    // neighbouring indices have similar lengths.  Wave w of a block runs on SIMD (w mod 4), so the block's
+    // waves are dealt in rounds of 4 (one per SIMD): wave w of block b takes the wave-set (64/G
+    // consecutive indices) r * 4 * gridDim.x + 4 * b + (w mod 4), r = w / 4.  The groups of a wave and
+    // the 4 SIMDs of a round get similar lengths; successive rounds (the waves sharing a SIMD) come from
+    // different parts of the order.  (Block b taking indices [b * groups, ...) gave the 16 waves of a
+    // 64-lane-plan block, 4 per SIMD, the 16 longest sequences of the batch: 1400.hmm x 8192 0.66 vs
+    // 0.46 ms, 1901.hmm x 256 0.44 vs 0.26 ms; dealing single groups over blocks put each block's
+    // longest sequences on one SIMD: cfg2 0.105 vs 0.185 ms -- profiles/r02_ab_first_assignment.jsonl.)
+    // Batches larger than the grid (the counter hands out the rest) keep block b on indices [b * groups,
+    // ...): there the first sequences all have about the same length, and the rounds measured 0.4-1%
+    // slower on cfg3/cfg5.
+    static_assert(WAVES % 4 == 0, "waves are dealt in rounds of one per SIMD");
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t wave_set = a.n <= n_groups ? (wave >> 2) * 4u * gridDim.x + 4u * blockIdx.x + (wave & 3u)
+                                              : blockIdx.x * WAVES + wave;
+    uint32_t pending = wave_set * (64 / G) + static_cast<uint32_t>(lane / G);
 
     using Ph0 = std::integral_constant<int, 0>;
     const uint32_t blk_lane = static_cast<uint32_t>(gl & (BLKN > 0 ? BLKN - 1 : 0));  // BLK: the lane's row in a block
