@@ -325,6 +325,35 @@ def main():
     host_streamed = streamed_rate()
     streamed_scores = outs[(args.steps - 1) % 2].copy()
 
+    # Information, never `value` (run BEFORE the timed steps, so those stay the last K MSV dispatches for
+    # tools/rocprof_window.py): K steps as a stream of resident batches alternating over two streams, so
+    # each step's blocks take the CUs that the previous step's drain tail frees (what
+    # msv_score_batch_async does for host batches).  Every step still sorts and scores its whole batch.
+    stream_b = torch.cuda.Stream(dev)
+    d_scores_b = torch.full_like(d_scores, float("nan"))
+    d_order_b = torch.empty_like(d_order)
+    lanes = [(stream, d_scores, d_order), (stream_b, d_scores_b, d_order_b)]
+
+    def step_two_streams(k):
+        st, sc, od = lanes[k % 2]
+        order_ptr = None
+        if not args.no_order:
+            engine.order_longest_first(d_off.data_ptr(), n, od.data_ptr(), st.cuda_stream)
+            order_ptr = od.data_ptr()
+        engine.score_batch_device(d_res.data_ptr(), residues, d_off.data_ptr(), n, sc.data_ptr(), order_ptr,
+                                  st.cuda_stream)
+
+    for k in range(2):
+        step_two_streams(k)
+    torch.cuda.synchronize(dev)
+    tb = time.perf_counter()
+    for k in range(args.steps):
+        step_two_streams(k)
+    torch.cuda.synchronize(dev)
+    two_stream_rate = residues * args.steps / (time.perf_counter() - tb) / 1e6
+    engine.check(sh)
+    two_stream_scores = (d_scores[:n].cpu().numpy().copy(), d_scores_b[:n].cpu().numpy().copy())
+
     for _ in range(args.warmup):
         step()
     engine.check(sh)  # raises on any latched kernel error
@@ -353,35 +382,6 @@ def main():
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
         residues_all = int(r[0])
 
-    # Information, never `value`: the same K steps as a stream of resident batches alternating over
-    # two streams, so each step's blocks take the CUs that the previous step's drain tail frees (what
-    # msv_score_batch_async does for host batches).  Every step still sorts and scores its whole batch.
-    stream_b = torch.cuda.Stream(dev)
-    d_scores_b = torch.full_like(d_scores, float("nan"))
-    d_order_b = torch.empty_like(d_order)
-    lanes = [(stream, d_scores, d_order), (stream_b, d_scores_b, d_order_b)]
-
-    def step_two_streams(k):
-        st, sc, od = lanes[k % 2]
-        order_ptr = None
-        if not args.no_order:
-            engine.order_longest_first(d_off.data_ptr(), n, od.data_ptr(), st.cuda_stream)
-            order_ptr = od.data_ptr()
-        engine.score_batch_device(d_res.data_ptr(), residues, d_off.data_ptr(), n, sc.data_ptr(), order_ptr,
-                                  st.cuda_stream)
-
-    for k in range(2):
-        step_two_streams(k)
-    torch.cuda.synchronize(dev)
-    tb = time.perf_counter()
-    for k in range(args.steps):
-        step_two_streams(k)
-    torch.cuda.synchronize(dev)
-    two_stream_rate = residues * args.steps / (time.perf_counter() - tb) / 1e6
-    engine.check(sh)
-    two_stream_same = bool(np.array_equal(d_scores_b[:n].cpu().numpy().view(np.uint32),
-                                          d_scores[:n].cpu().numpy().view(np.uint32)))
-
     # weak configs: output collection after timing (RCCL all-gather of every rank's scores)
     gather_ms = None
     if world > 1 and gathered is None:
@@ -397,7 +397,7 @@ def main():
     ok = ok and bool(np.array_equal(pinned_scores.view(np.uint32), scores.view(np.uint32)))
     ok = ok and bool(np.array_equal(pageable_scores.view(np.uint32), scores.view(np.uint32)))
     ok = ok and bool(np.array_equal(streamed_scores.view(np.uint32), scores.view(np.uint32)))
-    ok = ok and two_stream_same
+    ok = ok and all(bool(np.array_equal(x.view(np.uint32), scores.view(np.uint32))) for x in two_stream_scores)
     ok = ok and bool(np.array_equal(copy_scores.view(np.uint32), scores.view(np.uint32)))
     if gathered is not None and world > 1:  # every shard landed at its rows of the gathered set
         g = gathered.cpu().numpy().reshape(world, -1)
@@ -481,8 +481,8 @@ def main():
                         "kernel; rank 0, warm, mean of `steps` calls); host_pinned_copy_pipeline = the same "
                         "call with the residues copied in pieces under the kernels; host_pinned_streamed = the same batch as a stream of `steps` "
                         "msv_score_batch_async calls, two in flight (copy of one under the kernel of the "
-                        "other, kernels on alternating streams); resident_two_streams = the timed steps "
-                        "again, alternating over two streams so each step's blocks fill the previous "
+                        "other, kernels on alternating streams); resident_two_streams = `steps` resident "
+                        "steps before the timed ones, alternating over two streams so each step's blocks fill the previous "
                         "step's drain tail; `value` is the HBM-resident rate of serial steps the bench "
                         "contract prescribes",
             },
