@@ -25,6 +25,22 @@ def random_batch(seed: int, n: int, lmin: int, lmax: int) -> tuple[np.ndarray, n
     return codes, offsets
 
 
+# Amino-acid background frequencies in ACDEFGHIKLMNPQRSTVWY order: the reference's
+# background_frequencies (algorithms/MSV_HMM.cpp:21-27, HMMER3's standard p7_bg for amino acids).
+BACKGROUND = np.array([0.0787945, 0.0151600, 0.0535222, 0.0668298, 0.0397062, 0.0695071, 0.0229198,
+                       0.0590092, 0.0594422, 0.0963728, 0.0237718, 0.0414386, 0.0482904, 0.0395639,
+                       0.0540978, 0.0683364, 0.0540687, 0.0673417, 0.0114135, 0.0304133])
+
+
+def background_batch(seed: int, n: int, length: int) -> tuple[np.ndarray, np.ndarray]:
+    """n sequences of `length` residues drawn iid from BACKGROUND -- the null sequences HMMER3 scores to
+    calibrate a profile's STATS LOCAL MSV mu (p7_MSVMu: L = 200, iid from the background)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    codes = rng.choice(20, size=n * length, p=BACKGROUND / BACKGROUND.sum()).astype(np.uint8)
+    offsets = np.arange(0, n * length + 1, length, dtype=np.uint64)
+    return codes, offsets
+
+
 def write_fasta(path: str, codes: np.ndarray, offsets: np.ndarray, line: int = 70) -> None:
     """'> random i' headers, `line`-column residue lines (random_FASTA_generator.py:14-16)."""
     letters = np.frombuffer(AMINO_ACIDS.encode(), np.uint8)[codes].tobytes().decode()

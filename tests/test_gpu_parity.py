@@ -324,6 +324,26 @@ def test_score_grid_device_torch_stream():
         assert np.array_equal(bits(got[k]), bits(e.score_batch(codes=codes, offsets=offsets)))
 
 
+def test_pvalues_match_every_profiles_calibration():
+    """Statistical pin of the P-value pipeline on all 24 profiles: 20k iid background sequences of length
+    200 (what HMMER3's p7_MSVMu scores to fit STATS LOCAL MSV mu) scored on the GPU give P-values that
+    are ~uniform, and a Gumbel mu refitted to our bit scores (lambda fixed) lands within 0.75 bits of the
+    file's mu (measured -0.07 .. +0.50: the reference's float MSV scores slightly above HMMER's 8-bit
+    calibration filter; profiles/r02_pvalue_calibration.jsonl).  A unit, sign or null-model error would
+    miss by orders of magnitude."""
+    from hmm_fasta_viterbi_amd.synthetic import background_batch
+    codes, offsets = background_batch(2024, 20_000, 200)
+    for prof in PROFILES:
+        e = engine(prof)
+        pv = e.pvalues(e.score_batch(codes=codes, offsets=offsets), offsets)
+        mu, lam = e.msv_mu, e.msv_lambda
+        b = mu - np.log(-np.log1p(-pv)) / lam
+        mu_fit = -np.log(np.mean(np.exp(-lam * b))) / lam
+        assert abs(mu_fit - mu) < 0.75, (prof, mu, mu_fit)
+        for t in (0.5, 0.1, 0.01):
+            assert t / 2.5 < float(np.mean(pv < t)) < t * 2.5, (prof, t, float(np.mean(pv < t)))
+
+
 def test_pvalues_device_matches_host():
     """the device P-value kernel equals the host formula (float64 libm vs device
     libm: 1e-13 relative), on GPU scores of a seeded batch, and msv_filter's pass mask uses it."""

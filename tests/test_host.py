@@ -316,3 +316,28 @@ def test_msv_pvalues_gumbel_against_scipy():
         # scipy's sf = -expm1(-exp(-y)); the library's 1 - exp(-exp(-y)) loses relative precision only
         # where P is tiny, which the small-tail branch (P = exp(-y) when exp(-y) < 5e-9) covers
         np.testing.assert_allclose(out, want, rtol=1e-7, atol=1e-15)
+
+
+def test_msv_pvalues_against_the_profiles_own_calibration():
+    """The whole P-value pipeline (MSV score -> null1 -> bits -> Gumbel with the file's STATS LOCAL MSV)
+    checked statistically against the calibration HMMER3 stored in the reference's own .hmm fixtures:
+    HMMER fits mu to the MSV bit scores of iid background sequences of length 200 (p7_MSVMu), so our
+    P-values of such sequences must be ~uniform, and a Gumbel mu refitted to our bit scores (lambda
+    fixed, ML) must land on the file's mu.  The reference's float MSV scores ~0.0-0.5 bits above the
+    calibration (HMMER calibrates with its 8-bit MSV filter), so the bounds allow 0.75 bits and a factor
+    2.5 in the tail; a nats/bits, sign or null-model error moves these by orders of magnitude.  Scores
+    here are the oracle's (CPU, bit-identical to the GPU kernel); the GPU test repeats it at 20k."""
+    from hmm_fasta_viterbi_amd.synthetic import background_batch
+    for prof, seed in (("100.hmm", 11), ("400.hmm", 12)):
+        codes, offsets = background_batch(seed, 1500, 200)
+        sc = OracleProfile(prof).score_batch(codes, offsets)
+        e_h = msv.Profile_HMM(profile_path(prof))
+        mu, lam = e_h.stats_local_msv_mu, e_h.stats_local_msv_lambda
+        pv = np.zeros(len(sc), np.float64)
+        from hmm_fasta_viterbi_amd import _native
+        assert _native.lib().msv_pvalues(sc.ctypes.data, offsets.ctypes.data, len(sc), mu, lam, pv.ctypes.data) == 0
+        bits = mu - np.log(-np.log1p(-pv)) / lam  # invert the Gumbel survival: the bit scores used
+        mu_fit = -np.log(np.mean(np.exp(-lam * bits))) / lam
+        assert abs(mu_fit - mu) < 0.75, (prof, mu, mu_fit)
+        for t in (0.5, 0.1):
+            assert t / 2.5 < float(np.mean(pv < t)) < t * 2.5, (prof, t, float(np.mean(pv < t)))
