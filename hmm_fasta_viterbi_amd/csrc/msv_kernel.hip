@@ -182,7 +182,6 @@ template <int PF>
 struct RowCtx {
     static constexpr int kPF = PF;
     const float4* ep;
-    const float4* ep_next;  // XNEXT: the next row's LDS row, requested in this row's last PF chunks
     float Bt, nbr, p0, p1, p2, p3;  // (p2, p3 unused: keeping them keeps the register assignment measured in round 1)
     uint8_t rnext;   // residue code RPF rows ahead
     float4 ring[PF];
@@ -232,16 +231,6 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // chunks are requested right after this row's last cell update, so the LDS latency hides behind
     // the E butterfly and the specials instead of stalling the start of every row.
     constexpr bool XROW = !BIG && !SPLIT && D == 1 && PF >= C4 && St::RPF >= 2;
-    // Long rows (one residue of prefetch, a PF-chunk ring): the ring slots that the row's last PF chunks
-    // free are refilled with the NEXT row's first chunks (its residue was loaded at this row's start),
-    // so the next row starts on data that landed during this row's epilogue instead of waiting for
-    // its first LDS reads.  Off: with 4 waves per SIMD the row-start LDS wait is already covered by the
-    // other waves, and the ring's live range across the epilogue costs registers -- 16 x 88 -0.8..-1.1%,
-    // but 16 x 64/76/84/96 +0.5..+0.8% and 32 x 60 +3.7% (profiles/r02_ab_xnext.jsonl).
-#ifndef MSV_XNEXT
-#define MSV_XNEXT 0
-#endif
-    constexpr bool XNEXT = MSV_XNEXT && !XROW && !BIG && !SPLIT && D == 1 && St::RPF == 1;
     // ... and two rows ahead when the residue slots rotate over an even number of phases: rows of
     // even and odd phase keep their own ring, refilled with the row after next right after use, so
     // the LDS reads have a whole row to land instead of the epilogue's dozen instructions (cfg2:
@@ -446,7 +435,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             rc.nbr = shift_in<G>(st.M[S - 1], NINF);
         }
         // p0/p1 start from the row's first chunk (a plain max, no -inf seed)
-        if constexpr (!XROW && !XNEXT) fill_ring(rc, ep);
+        if constexpr (!XROW) fill_ring(rc, ep);
     };
     // One float4 chunk (states 4c+1 .. 4c+4 of the lane), highest state first so M[k-1] is still
     // the previous row's value; the next chunk is requested PF chunks ahead.
@@ -455,12 +444,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         constexpr int c = decltype(cc)::value;
         constexpr int slot = (CA - 1 - c) % P;
         const float4 ev = rc.ring[slot];
-        if constexpr (c - P >= 0) {
-            rc.ring[slot] = rc.ep[(c - P) * G];
-        } else if constexpr (XNEXT) {  // this row's last chunks: the next row's chunk CA-1-slot into the slot
-            if constexpr (c == P - 1 || (P > CA && c == CA - 1)) rc.ep_next = lds_row(rc.rnext);
-            rc.ring[slot] = rc.ep_next[(CA - 1 - slot) * G];
-        }
+        if constexpr (c - P >= 0) rc.ring[slot] = rc.ep[(c - P) * G];
         constexpr int k = 4 * c;
         if constexpr (!BIG && S >= 64) {
             // The chunk's 10 VALU ops in a fixed interleaved order (max, max, add, max, add, max, add,
@@ -609,7 +593,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
     // the LDS-row class for G = 64 -- measured no gain, and 15% LOSS for the latter on 2405.hmm.)
 
     RowCtx<PF> xr, xr1;  // XROW: the ring persists across rows (XROW2: xr for even phases, xr1 for odd)
-    if constexpr (XROW || XNEXT) fill_ring(xr, row_ptr(s0, Ph0{}));
+    if constexpr (XROW) fill_ring(xr, row_ptr(s0, Ph0{}));
     if constexpr (XROW2) fill_ring(xr1, lds_row(resid(s0, std::integral_constant<int, 1>{})));
     fill_b(s0.r[0]);
 
@@ -715,8 +699,6 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
                     RowCtx<(C4 < 10 ? C4 : 10)> c0;
                     row(s0, c0, &a.etab[rr * ROW_F4 + gl], Ph0{});
                 }
-            } else if constexpr (D == 1 && XNEXT) {
-                row(s0, xr, row_ptr(s0, Ph0{}), Ph0{});  // the ring persists: filled by the row before
             } else if constexpr (D == 1) {
                 RowCtx<PF> c0;
                 row(s0, c0, row_ptr(s0, Ph0{}), Ph0{});
@@ -751,7 +733,6 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
                 if (s0.pos == s0.endp) {
                     finish(s0, Ph0{});
                     fill_b(s0.r[0]);
-                    if constexpr (XNEXT) fill_ring(xr, row_ptr(s0, Ph0{}));  // the new sequence's first row
                 }
                 if constexpr (D == 2) {
                     if (s1.pos == s1.endp) finish(s1, Ph0{});
