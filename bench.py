@@ -260,17 +260,32 @@ def main():
     sh = stream.cuda_stream
     engine.reserve_length(lmax)
     engine.bind_stream(sh)  # the bench's stream outlives every launch of this engine
+    from hmm_fasta_viterbi_amd import _native
+    native = _native.lib()
+    native.msv_debug_time_next_launch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    hip = C.CDLL("libamdhip64.so.7")  # torch's HIP runtime (already loaded: one runtime per process)
+    hip.hipEventCreate.argtypes = [C.POINTER(C.c_void_p)]
+    hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
+    hip.hipEventDestroy.argtypes = [C.c_void_p]
+
+    def hip_event():
+        e = C.c_void_p()
+        assert hip.hipEventCreate(C.byref(e)) == 0
+        return e.value
+
+    def hip_elapsed_ms(a, b):
+        ms = C.c_float()
+        assert hip.hipEventElapsedTime(C.byref(ms), a, b) == 0
+        return float(ms.value)
 
     def step(ev=None):
         order_ptr = None
         if not args.no_order:
             engine.order_longest_first(d_off.data_ptr(), n, d_order.data_ptr(), sh)
             order_ptr = d_order.data_ptr()
-        if ev is not None:
-            ev[0].record(stream)
+        if ev is not None:  # the MSV launch itself updates these two HIP events (hipExtLaunchKernel)
+            native.msv_debug_time_next_launch(engine._p, ev[0], ev[1])
         engine.score_batch_device(d_res.data_ptr(), residues, d_off.data_ptr(), n, d_scores.data_ptr(), order_ptr, sh)
-        if ev is not None:
-            ev[1].record(stream)
         if gathered is not None and world > 1:  # cfg4: the RCCL gather of the scores is part of the step
             with torch.cuda.stream(stream):
                 src = d_scores if backend == "nccl" else d_scores.cpu()
@@ -299,7 +314,6 @@ def main():
                                            settle_s=0.5)
     host_pageable, pageable_scores = host_rate(codes, np.zeros(n, np.float32))
     # pinned residues are read in place by the kernel (zero-copy); the same call through the copy pipeline:
-    from hmm_fasta_viterbi_amd import _native
     _native.lib().msv_debug_set_zero_copy.argtypes = [C.c_void_p, C.c_int]
     _native.lib().msv_debug_set_zero_copy(engine._p, 0)
     host_pinned_copy, copy_scores = host_rate(pinned_codes, torch.empty(n, dtype=torch.float32).pin_memory().numpy())
@@ -359,7 +373,10 @@ def main():
     engine.check(sh)  # raises on any latched kernel error
     torch.cuda.synchronize(dev)
 
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # Kernel timing: HIP events that the MSV launch updates with its own start and end (hipExtLaunchKernel on
+    # the launch stream), not event records around it -- each record is a marker packet (~4 us in the
+    # stream), which would add ~8 us to every step (7% of cfg2's).
+    events = [(hip_event(), hip_event()) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -372,7 +389,10 @@ def main():
     t1 = time.perf_counter()
     engine.check(sh)
     elapsed = t1 - t0
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    kernel_ms = float(np.mean([hip_elapsed_ms(a, b) for a, b in events]))
+    for a, b in events:
+        hip.hipEventDestroy(a)
+        hip.hipEventDestroy(b)
     residues_all = residues
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=cdev)

@@ -265,6 +265,7 @@ struct msv_profile {
     uint32_t* d_order = nullptr;  // msv_score_fasta_device's longest-first order
     size_t d_order_cap = 0;
     uint64_t* d_stamps = nullptr;  // diagnostic timeline buffer (tools only), or nullptr
+    hipEvent_t time_start = nullptr, time_stop = nullptr;  // msv_debug_time_next_launch (one launch)
     hipEvent_t done = nullptr;     // grid API: joins this profile's stream back to the caller's
 };
 
@@ -652,6 +653,16 @@ msv_status msv_debug_set_pipeline(msv_profile* p, uint32_t first_den, uint32_t g
     return MSV_OK;
 }
 
+// Diagnostics (not in msv.h): the profile's next MSV launch updates `start` / `stop` (hipEvent_t, created
+// with timing) with its own start and end through hipExtLaunchKernel -- the kernel duration without the
+// two marker packets (~4 us each on the stream) that event records around the launch would add.
+msv_status msv_debug_time_next_launch(msv_profile* p, void* start, void* stop) {
+    if (!p) return MSV_ERR_INVALID_ARGUMENT;
+    p->time_start = static_cast<hipEvent_t>(start);
+    p->time_stop = static_cast<hipEvent_t>(stop);
+    return MSV_OK;
+}
+
 // Diagnostics (not in msv.h): msv_score_batch reads page-locked residues in place (1, default) or
 // copies them through the piece pipeline like pageable ones (0).
 msv_status msv_debug_set_zero_copy(msv_profile* p, int on) {
@@ -740,7 +751,9 @@ static msv_status launch_batch(msv_profile* p, const uint8_t* d_residues, uint64
     a.errors = d_errors ? d_errors : p->d_words + kErrWord;
     if (p->kernels.dirty[k]) MSV_HIP(hipMemsetAsync(a.counter, 0, 2 * sizeof(uint32_t), st));
     p->kernels.dirty[k] = true;
-    MSV_HIP(msvk::launch_variant(*plan.v, dim3(blocks), a, st));
+    hipEvent_t t0 = p->time_start, t1 = p->time_stop;
+    p->time_start = p->time_stop = nullptr;
+    MSV_HIP(msvk::launch_variant(*plan.v, dim3(blocks), a, st, t0, t1));
     p->kernels.dirty[k] = false;
     MSV_HIP(p->kernels.release(k, st, lazy_stream(p, st)));
     return MSV_OK;

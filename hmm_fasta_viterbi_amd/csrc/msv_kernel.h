@@ -45,7 +45,10 @@ struct Variant {
 };
 
 const Variant* variants(int* count);
-hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, hipStream_t stream);
+// start/stop (optional): events updated with the kernel's own start and end (hipExtLaunchKernel), so a
+// timed launch costs no extra marker packets on the stream.
+hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, hipStream_t stream,
+                          hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t n, float mu, float lambda,
                           double* pvalues, hipStream_t stream);
 

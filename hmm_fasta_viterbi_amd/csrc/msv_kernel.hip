@@ -38,6 +38,7 @@
 //     1-6 rows of prefetch into rotating slots, by row length); the per-length transition
 //     constants come from a host-computed table (host logf, so scores never depend on a device
 //     logf).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -900,8 +901,10 @@ const Variant* variants(int* count) {
     return kVariants;
 }
 
-hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, hipStream_t stream) {
+hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, hipStream_t stream, hipEvent_t start,
+                          hipEvent_t stop) {
     void* params[] = {const_cast<KernelArgs*>(&args)};
+    if (start || stop) return hipExtLaunchKernel(v.fn, grid, dim3(v.waves * 64), params, 0, stream, start, stop, 0);
     return hipLaunchKernel(v.fn, grid, dim3(v.waves * 64), params, 0, stream);
 }
 
