@@ -48,6 +48,32 @@ def device_count() -> int:
     return n.value
 
 
+class _HostBuffer:
+    """Owner of one msv_host_alloc block; freed when the last numpy view of it goes away."""
+
+    def __init__(self, nbytes: int):
+        self.ptr = C.c_void_p()
+        check(_native.lib().msv_host_alloc(max(int(nbytes), 1), C.byref(self.ptr)), "msv_host_alloc")
+        self.nbytes = int(nbytes)
+
+    def __del__(self):
+        lib = _loaded_lib()
+        if lib is not None and self.ptr:
+            lib.msv_host_free(self.ptr)
+            self.ptr = C.c_void_p()
+
+
+def pinned_empty(shape, dtype=np.uint8) -> np.ndarray:
+    """A numpy array in page-locked host memory (msv_host_alloc).  score_batch reads residues from such
+    an array in place on the GPU (no staging copy) and writes scores into one directly."""
+    dt = np.dtype(dtype)
+    count = int(np.prod(shape)) if np.ndim(shape) else int(shape)
+    owner = _HostBuffer(count * dt.itemsize)
+    raw = (C.c_uint8 * max(owner.nbytes, 1)).from_address(owner.ptr.value)
+    raw.owner = owner  # every view keeps `raw` (its base), `raw` keeps the allocation
+    return np.frombuffer(raw, dtype=dt, count=count).reshape(shape)
+
+
 def sequence_transitions(L: int) -> tuple[float, float]:
     """(tr_loop, tr_move) of MSV_HMM::init_transitions_depend_on_seq (MSV_HMM.cpp:59-64)."""
     a, b = C.c_float(), C.c_float()
@@ -174,8 +200,9 @@ class MSV_HMM:
     # -- batch API --------------------------------------------------------------------------
     def score_batch(self, seqs: Sequence[str] | None = None, *, codes: np.ndarray | None = None,
                     offsets: np.ndarray | None = None, out: np.ndarray | None = None) -> np.ndarray:
-        """Scores of a host batch (msv_score_batch).  `out`: optional float32[n] destination (e.g. a
-        pinned array, torch pin_memory().numpy(), so the scores' D2H needs no runtime staging)."""
+        """Scores of a host batch (msv_score_batch).  Page-locked `codes` (msv.pinned_empty, torch
+        pin_memory().numpy()) are read by the kernel in place, with no staging copy; a page-locked `out`
+        (float32[n]) is written by the kernel directly."""
         if seqs is not None:
             codes, offsets = pack_sequences(seqs)
         codes = np.ascontiguousarray(codes, np.uint8)

@@ -817,6 +817,18 @@ msv_status msv_order_longest_first(msv_profile* p, const uint64_t* d_offsets, ui
     return MSV_OK;
 }
 
+msv_status msv_host_alloc(size_t bytes, void** out) {
+    if (!out) return MSV_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    MSV_HIP(hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocPortable));
+    return MSV_OK;
+}
+
+msv_status msv_host_free(void* ptr) {
+    if (ptr) MSV_HIP(hipHostFree(ptr));
+    return MSV_OK;
+}
+
 msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
                            float* scores, void* stream) {
     if (!p || (n && (!offsets || !scores))) return MSV_ERR_INVALID_ARGUMENT;

@@ -166,6 +166,14 @@ msv_status msv_profile_set_variant(msv_profile* profile, const char* name);
  * scored (default 131072). Host logf values, so the device never evaluates logf. */
 msv_status msv_profile_reserve_length(msv_profile* profile, uint64_t max_length);
 
+/* Page-locked host memory (visible to every GPU).  Residues and scores in such buffers are read and
+ * written by the kernels in place (msv_score_batch: no staging copy, ~0.93 of the HBM-resident rate on
+ * the BASELINE configs) -- the allocator for FFI callers that cannot reach hipHostMalloc.  Release with
+ * msv_host_free.  (Any page-locked memory works the same: hipHostMalloc, hipHostRegister, torch
+ * pin_memory.) */
+msv_status msv_host_alloc(size_t bytes, void** out);
+msv_status msv_host_free(void* ptr);
+
 /* Host buffers in, host scores out; synchronous.  n = number of sequences; offsets has n+1
  * entries, offsets[0] may be non-zero.  scores[s] = MSV log-odds score of sequence s, exactly
  * MSV_HMM::run_on_sequence (MSV_HMM.cpp:74-113); an empty sequence scores -inf.

@@ -139,6 +139,41 @@ int main(int argc, char** argv) {
             }
         checked += static_cast<int>(want.size());
     }
+    // page-locked buffers from msv_host_alloc: residues read in place by the kernel, scores written by it
+    // (the FFI caller's zero-copy path) -- equal to the pageable path
+    {
+        auto m = MSV_HMM(Profile_HMM(root + "/data/profile_HMMs/1400.hmm"));
+        const size_t n = fasta.sequences.size();
+        std::vector<uint8_t> codes;
+        std::vector<uint64_t> offs(1, 0);
+        for (const auto& s : fasta.sequences) {  // '#' + residues, as the reference stores them
+            std::vector<uint8_t> c(s.size() - 1);
+            if (msv_encode_residues(s.c_str() + 1, s.size() - 1, c.data()) != MSV_OK) return 1;
+            codes.insert(codes.end(), c.begin(), c.end());
+            offs.push_back(codes.size());
+        }
+        void *pc = nullptr, *ps = nullptr;
+        if (msv_host_alloc(codes.size(), &pc) != MSV_OK || msv_host_alloc(n * sizeof(float), &ps) != MSV_OK) {
+            std::printf("test_msv failed! msv_host_alloc\n");
+            return 1;
+        }
+        std::memcpy(pc, codes.data(), codes.size());
+        std::vector<float> want(n);
+        if (msv_score_batch(m.handle(), codes.data(), offs.data(), n, want.data(), nullptr) != MSV_OK ||
+            msv_score_batch(m.handle(), static_cast<uint8_t*>(pc), offs.data(), n, static_cast<float*>(ps),
+                            nullptr) != MSV_OK) {
+            std::printf("test_msv failed! msv_score_batch on pinned buffers\n");
+            return 1;
+        }
+        for (size_t i = 0; i < n; ++i)
+            if (!same_bits(static_cast<float*>(ps)[i], want[i])) {
+                std::printf("test_msv failed! pinned seq %zu: %a vs %a\n", i, static_cast<float*>(ps)[i], want[i]);
+                return 1;
+            }
+        msv_host_free(pc);
+        msv_host_free(ps);
+        checked += static_cast<int>(n);
+    }
     // error behaviour: a residue outside the 20 throws std::out_of_range like amino_acid_num.at
     auto msv = MSV_HMM(Profile_HMM(root + "/data/profile_HMMs/100.hmm"));
     bool threw = false;

@@ -313,6 +313,30 @@ def test_zero_copy_pinned_residues():
     e.close()
 
 
+def test_pinned_empty_arrays_zero_copy():
+    """msv.pinned_empty (msv_host_alloc): page-locked numpy arrays for residues and scores -- read and
+    written by the kernel in place -- give the pageable path's bits; the memory is released with the
+    last view (msv_host_free)."""
+    import gc
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("900.hmm")))
+    codes, offsets = random_batch(530, 20_000, 1, 700)
+    want = e.score_batch(codes=codes, offsets=offsets)
+    for _ in range(3):  # allocate / release repeatedly
+        pc = msv.pinned_empty(codes.shape, np.uint8)
+        pc[:] = codes
+        out = msv.pinned_empty(len(want), np.float32)
+        got = e.score_batch(codes=pc, offsets=offsets, out=out)
+        assert got is out and np.array_equal(bits(out), bits(want))
+        view = pc[int(offsets[10]):]
+        del pc, out, got
+        gc.collect()
+        sub = e.score_batch(codes=view, offsets=(offsets[10:] - offsets[10]).astype(np.uint64))
+        assert np.array_equal(bits(sub), bits(want[10:]))  # the view alone keeps the allocation alive
+        del view
+        gc.collect()
+    e.close()
+
+
 def test_rccl_multi_device_context():
     """msv_multi_*: ncclCommInitAll over the given devices, shards scored per device, scores gathered
     into device 0 by ONE grouped ncclSend/ncclRecv (rank 0 through a self send/recv), one D2H.  On a
