@@ -288,6 +288,29 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
                                               : blockIdx.x * WAVES + wave;
     uint32_t pending = wave_set * (64 / G) + static_cast<uint32_t>(lane / G);
 
+#ifndef MSV_YOUNG_CUTOFF
+#define MSV_YOUNG_CUTOFF 8
+#endif
+    // Drain tail.  The waves of a block are arbitrated oldest-first on their SIMD, so the youngest
+    // quarter issue last: a sequence they take near the end of the queue finishes last and sets the
+    // launch's end (cfg3 timeline: waves 12-15 did a fifth of the rows of waves 0-3 and still ended
+    // 90 us after them -- profiles/r02_wave_timeline_cfg3.jsonl).  For large profiles (S >= 64, whose
+    // rows are long enough that fewer waves still keep the SIMD issuing) those waves stop taking
+    // sequences once fewer than n_groups * MSV_YOUNG_CUTOFF / 4 remain and leave them to the older
+    // waves: cfg3 2.93 -> 2.88 ms, the other large profiles within 0.3%.  Small profiles stay
+    // issue-bound to the end (cfg2 lost 9%), so they keep every wave -- profiles/r02_ab_young_cutoff.jsonl.
+    constexpr uint32_t kYoung = S >= 64 ? MSV_YOUNG_CUTOFF : 0;
+    const bool young = kYoung > 0 && (threadIdx.x >> 6) >= (3u * WAVES) / 4u;
+    auto take = [&]() __attribute__((always_inline)) -> uint32_t {
+        if constexpr (kYoung > 0) {
+            if (young) {
+                const uint32_t cur = group_take<G>(a.counter, false, lane, n_groups);  // +0: a read
+                if (static_cast<uint64_t>(cur) + (static_cast<uint64_t>(n_groups) * kYoung) / 4 >= a.n)
+                    return 0xFFFFFFFEu;  // >= n: retire
+            }
+        }
+        return group_take<G>(a.counter, leader, lane, n_groups);
+    };
     using Ph0 = std::integral_constant<int, 0>;
     const uint32_t blk_lane = static_cast<uint32_t>(gl & (BLKN > 0 ? BLKN - 1 : 0));  // BLK: the lane's row in a block
 
@@ -301,7 +324,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         // on neutral state and discarded, and the stream then restarts with the next index.
         uint32_t idx = pending;
         pending = kNone;
-        if (idx == kNone) idx = group_take<G>(a.counter, leader, lane, n_groups);
+        if (idx == kNone) idx = take();
         const bool retire = idx >= a.n;
         uint32_t s = 0;
         uint64_t o0 = 0, o1 = 0;
@@ -657,7 +680,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
         // Events: see the generic loop below.
         if (G == 64 || __any(s0.pos == s0.ev)) {
             if (s0.pos == s0.ev && s0.ev != s0.endp) {
-                if (pending == kNone) pending = group_take<G>(a.counter, leader, lane, n_groups);
+                if (pending == kNone) pending = take();
                 s0.ev = s0.endp;
             }
             if (s0.pos == s0.endp) {
@@ -722,12 +745,12 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
             // left out.)
             if (G == 64 || __any(D == 2 ? (s0.pos == s0.ev || s1.pos == s1.ev) : s0.pos == s0.ev)) {
                 if (s0.pos == s0.ev && s0.ev != s0.endp) {
-                    if (pending == kNone) pending = group_take<G>(a.counter, leader, lane, n_groups);
+                    if (pending == kNone) pending = take();
                     s0.ev = s0.endp;
                 }
                 if constexpr (D == 2) {
                     if (s1.pos == s1.ev && s1.ev != s1.endp) {
-                        if (pending == kNone) pending = group_take<G>(a.counter, leader, lane, n_groups);
+                        if (pending == kNone) pending = take();
                         s1.ev = s1.endp;
                     }
                 }
