@@ -74,12 +74,16 @@ class KernelInfo(C.Structure):
         ("latency_variant", C.c_char * 64),
         ("latency_blocks", C.c_uint32),
         ("latency_max_n", C.c_uint64),
+        ("mid_variant", C.c_char * 64),
+        ("mid_blocks", C.c_uint32),
+        ("mid_max_n", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
         d = {f: getattr(self, f) for f, _ in self._fields_}
         d["variant"] = self.variant.decode()
         d["latency_variant"] = self.latency_variant.decode()
+        d["mid_variant"] = self.mid_variant.decode()
         return d
 
 

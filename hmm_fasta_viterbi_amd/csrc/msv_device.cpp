@@ -125,6 +125,20 @@ const msvk::Variant* pick_latency_variant(uint32_t states) {
     return best;
 }
 
+// Mid plan for batches between the latency plan's and one round of the main grid: two sequences per
+// wave (G = 32), the cheapest plain (LDS-table, one-stream) variant covering the model.
+const msvk::Variant* pick_mid_variant(uint32_t states) {
+    int count = 0;
+    const msvk::Variant* all = msvk::variants(&count);
+    const msvk::Variant* best = nullptr;
+    for (int i = 0; i < count; ++i) {
+        const msvk::Variant& v = all[i];
+        if (v.G != 32 || v.streams != 1 || v.big || v.sa || static_cast<uint32_t>(v.G * v.S) < states) continue;
+        if (!best || variant_cost(v) < variant_cost(*best)) best = &v;
+    }
+    return best;
+}
+
 const msvk::Variant* pick_variant(uint32_t states) {
     int count = 0;
     const msvk::Variant* all = msvk::variants(&count);
@@ -212,8 +226,10 @@ struct msv_profile {
     uint32_t model_length = 0;  // LENG + 1
     Plan main;                    // throughput plan (every launch unless the batch is small)
     Plan lat;                     // latency plan for small batches (G = 64), may equal main's variant
+    Plan mid;                     // mid-size batches (G = 32), large G = 16 profiles only
     bool force = false;           // msv_profile_set_variant: main plan for every batch size
     uint64_t lat_max_n = 0;       // batches up to this many sequences take the latency plan
+    uint64_t mid_max_n = 0;       // batches above lat_max_n and up to this many take the mid plan
     float tr_B_Mk = 0, tr_E_C = 0, tr_E_J = 0;
     std::vector<float> emission_scores;  // host copy [20][model_length] (for re-layout)
     float2* d_lentab = nullptr;
@@ -383,6 +399,38 @@ static msv_status install_plan(msv_profile* p, const msvk::Variant* v, Plan& pla
     return MSV_OK;
 }
 
+static void drop_plan(Plan& plan) {
+    if (plan.d_etab) {  // may be read by an in-flight launch
+        (void)hipDeviceSynchronize();
+        (void)hipFree(plan.d_etab);
+    }
+    plan = Plan{};
+}
+
+// Mid plan (G = 32, two sequences per wave) for the large G = 16 profiles (S >= 64, ~1000-1536
+// states), taken by batches above 1.5 rounds of the latency grid and below 0.9 of one round of the
+// main grid.  There a 16-lane launch runs one partial round of 400-row sequences at ~2-3 waves per
+// SIMD (latency-bound: ~4 ns per instruction per wave), and a 64-lane one needs 2-3 rounds; the
+// 32-lane rows are half as long as the 16-lane ones at twice the waves.  1400.hmm x U[300,500]:
+// 9000 sequences 0.388 ms against 0.458 (latency plan) / 0.527 (main), 12000 0.464 vs 0.536 (main);
+// 1001/1200/1509.hmm alike; at 6000 the latency plan and at 16000 the main plan are as fast or faster
+// (profiles/r02_mid_plans.jsonl).  Smaller profiles measured no consistent gain (500/700.hmm: the
+// 32-lane plan won at some sizes and lost 10-15% at others), so they keep two plans.
+static msv_status install_mid(msv_profile* p) {
+    const msvk::Variant* mv = pick_mid_variant(p->model_length - 1);
+    if (!mv || !p->lat.v || p->main.v->G != 16 || p->main.v->S < 64) return MSV_OK;
+    const uint64_t lat_cap = static_cast<uint64_t>(p->lat.blocks) * p->lat.groups_per_block;
+    const uint64_t main_cap = static_cast<uint64_t>(p->main.blocks) * p->main.groups_per_block;
+    const uint64_t lat_max = std::min<uint64_t>(p->lat_max_n, lat_cap * 3 / 2);
+    const uint64_t mid_max = main_cap * 9 / 10;
+    if (mid_max <= lat_max) return MSV_OK;
+    msv_status s = install_plan(p, mv, p->mid);
+    if (s != MSV_OK) return s;
+    p->lat_max_n = lat_max;
+    p->mid_max_n = mid_max;
+    return MSV_OK;
+}
+
 // Main plan for `v`, and the latency plan (its own table layout) unless it would be the same kernel.
 static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
     msv_status s = install_plan(p, v, p->main);
@@ -395,17 +443,17 @@ static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
     // r02_latency_plans.jsonl).
     const double main_row = 2.5 * v->S + 26.0, lat_row = lv ? 2.5 * lv->S + 36.0 + (lv->sa ? 2.0 : 0.0) : 0.0;
     const double ratio = lv ? main_row / lat_row : 0.0;
+    drop_plan(p->mid);
+    p->mid_max_n = 0;
     if (!lv || lv == v || ratio < 1.3) {
-        if (p->lat.d_etab) {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(p->lat.d_etab);
-        }
-        p->lat = Plan{};
+        drop_plan(p->lat);
         p->lat_max_n = 0;
         return MSV_OK;
     }
     p->lat_max_n = static_cast<uint64_t>(std::min(12288.0, 4096.0 * ratio));
-    return install_plan(p, lv, p->lat);
+    s = install_plan(p, lv, p->lat);
+    if (s != MSV_OK) return s;
+    return install_mid(p);
 }
 
 // Pieces of a host batch for msv_score_batch's copy/compute pipeline: cut[k] .. cut[k+1] is piece
@@ -503,6 +551,7 @@ void msv_profile_destroy(msv_profile* p) {
     (void)hipDeviceSynchronize();
     (void)hipFree(p->main.d_etab);
     (void)hipFree(p->lat.d_etab);
+    (void)hipFree(p->mid.d_etab);
     (void)hipFree(p->d_lentab);
     (void)hipFree(p->d_words);
     (void)hipFree(p->d_hist);
@@ -674,7 +723,8 @@ msv_status msv_debug_set_zero_copy(msv_profile* p, int on) {
 int msv_debug_grid_waves(const msv_profile* p) {
     if (!p) return 0;
     const int lat = p->lat.v ? p->lat.blocks * p->lat.v->waves : 0;
-    return std::max(p->main.blocks * p->main.v->waves, lat);  // the stamps buffer must fit either plan
+    const int mid = p->mid.v ? p->mid.blocks * p->mid.v->waves : 0;
+    return std::max({p->main.blocks * p->main.v->waves, lat, mid});  // the stamps buffer must fit every plan
 }
 
 msv_status msv_profile_create_from_hmm(int device, const msv_hmm* hmm, msv_profile** out) {
@@ -707,6 +757,11 @@ msv_status msv_profile_describe(const msv_profile* p, msv_kernel_info* out) {
         out->latency_blocks = static_cast<uint32_t>(p->lat.blocks);
         out->latency_max_n = p->lat_max_n;
     }
+    if (p->mid.v) {
+        std::snprintf(out->mid_variant, sizeof(out->mid_variant), "%s", p->mid.v->name);
+        out->mid_blocks = static_cast<uint32_t>(p->mid.blocks);
+        out->mid_max_n = p->mid_max_n;
+    }
     return MSV_OK;
 }
 
@@ -725,8 +780,12 @@ static msv_status launch_batch(msv_profile* p, const uint8_t* d_residues, uint64
 
     msvk::KernelArgs a{};
     // Small batches take the latency plan: with fewer sequences than ~4 per SIMD the launch lasts
-    // one sequence's rows, and a 64-lane row is far shorter than a 16-lane one.
-    const Plan& plan = (latency_ok && p->lat.v && n <= p->lat_max_n) ? p->lat : p->main;
+    // one sequence's rows, and a 64-lane row is far shorter than a 16-lane one.  Mid-size ones (less
+    // than one round of the main grid) take the 32-lane plan where there is one (install_variant).
+    const Plan& plan = !latency_ok                            ? p->main
+                       : (p->lat.v && n <= p->lat_max_n)      ? p->lat
+                       : (p->mid.v && n <= p->mid_max_n)      ? p->mid
+                                                              : p->main;
     a.etab = plan.d_etab;
     a.residues = residues_len ? d_residues : p->d_dummy;
     a.offsets = d_offsets;

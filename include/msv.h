@@ -148,10 +148,13 @@ typedef struct msv_kernel_info {
     uint32_t blocks;           /* workgroups per launch (persistent grid)            */
     uint32_t max_length;       /* longest sequence the transition table covers        */
     int device;
-    char variant[64];          /* throughput plan: every batch above latency_max_n sequences */
+    char variant[64];          /* throughput plan: batches above latency_max_n and mid_max_n */
     char latency_variant[64];  /* small-batch plan (one sequence per wave), "" if none      */
     uint32_t latency_blocks;   /* its persistent grid                                    */
     uint64_t latency_max_n;    /* batches of up to this many sequences take it            */
+    char mid_variant[64];      /* mid-size plan (two sequences per wave), "" if none        */
+    uint32_t mid_blocks;       /* its persistent grid                                    */
+    uint64_t mid_max_n;        /* batches above latency_max_n, up to this many, take it   */
 } msv_kernel_info;
 msv_status msv_profile_describe(const msv_profile* profile, msv_kernel_info* out);
 

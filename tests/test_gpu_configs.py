@@ -188,13 +188,19 @@ def test_score_batch_multi_same_handle_twice():
     b.close()
 
 
-def test_describe_reports_both_plans():
+def test_describe_reports_every_plan():
     e = msv.MSV_HMM(msv.Profile_HMM(profile_path("1400.hmm")))
     d = e.describe()
     assert d["latency_variant"].startswith("msv_g64_") and d["latency_max_n"] >= 4096
     assert d["latency_blocks"] > 0 and d["variant"] != d["latency_variant"]
+    # mid-size batches of a large G = 16 profile: the 32-lane plan, above the latency plan's range
+    assert d["mid_variant"].startswith("msv_g32_") and d["mid_blocks"] > 0
+    assert d["latency_max_n"] < d["mid_max_n"] < d["blocks"] * 64
     small = msv.MSV_HMM(msv.Profile_HMM(profile_path("100.hmm"))).describe()
     assert small["latency_variant"] == "" and small["latency_max_n"] == 0
+    assert small["mid_variant"] == "" and small["mid_max_n"] == 0
+    g32 = msv.MSV_HMM(msv.Profile_HMM(profile_path("1901.hmm"))).describe()  # main plan already 32 lanes
+    assert g32["lanes_per_group"] == 32 and g32["mid_variant"] == ""
     e.close()
 
 

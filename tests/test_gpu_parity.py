@@ -611,6 +611,27 @@ def test_latency_plan_small_batches_match_main_plan(prof):
     forced.close()
 
 
+@pytest.mark.parametrize("prof", ["1001", "1400", "1509"])
+def test_mid_plan_batches_match_main_plan(prof):
+    """Batches between the latency plan's limit and one round of the main grid run the 32-lane mid
+    plan (large G = 16 profiles); random and homolog sequences (J >= N rows), empty ones included,
+    give the main plan's bits and the oracle's."""
+    auto = msv.MSV_HMM(msv.Profile_HMM(profile_path(prof + ".hmm")))
+    d = auto.describe()
+    assert d["mid_variant"].startswith("msv_g32_") and d["latency_max_n"] < d["mid_max_n"]
+    n = (d["latency_max_n"] + d["mid_max_n"]) // 2
+    hc, ho = homolog_batch(msv.Profile_HMM(profile_path(prof + ".hmm")).match_emissions, 131, 200, 0, 600)
+    codes, offsets = concat_batches(random_batch(130, n - 200, 0, 800), (hc, ho))
+    got = auto.score_batch(codes=codes, offsets=offsets)
+    forced = msv.MSV_HMM(msv.Profile_HMM(profile_path(prof + ".hmm")))
+    forced.set_variant(d["variant"])
+    assert np.array_equal(bits(got), bits(forced.score_batch(codes=codes, offsets=offsets)))
+    sample = np.concatenate([np.arange(0, n, n // 40), np.arange(n - 200, n, 10)])
+    assert np.array_equal(bits(got[sample]), bits(OracleProfile(prof).score_batch(*subset(codes, offsets, sample))))
+    auto.close()
+    forced.close()
+
+
 def test_score_batch_multi_concurrent_length_table_growth():
     """Each shard holds a sequence longer than the default length table, so every host thread of
     msv_score_batch_multi grows its profile's table at once (shared host cache under a lock)."""
