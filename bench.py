@@ -247,6 +247,9 @@ def main():
         width = max(b - a for a, b in bounds)  # gather pads every shard to the largest
         del all_codes
     n = len(offsets) - 1
+    # the plan this batch size runs (latency / mid / throughput, msv_device.cpp select_plan)
+    variant = engine.variant_for(n)
+    var_g, var_s = (int(x[1:]) for x in variant.split("_")[1:3])
     residues = int(offsets[-1])
     d_res = torch.from_numpy(codes).to(dev)
     d_off = torch.from_numpy(offsets.view(np.int64)).to(dev)
@@ -429,7 +432,7 @@ def main():
     if rank == 0:
         cells_per_launch = residues * leng
         achieved = 3.0 * cells_per_launch / (kernel_ms * 1e-3) / 1e12
-        alg_bytes = residues + n * (8 + 8 + 4 + 4) + 21 * info["lanes_per_group"] * info["states_per_lane"] * 4
+        alg_bytes = residues + n * (8 + 8 + 4 + 4) + 21 * var_g * var_s * 4
         traffic = pmc_traffic(args.config)
         ceiling = issue_ceiling_tcells()
         per = "per GPU" if scaling == "weak" else f"in one set, {world} residue-balanced shard(s)"
@@ -456,7 +459,7 @@ def main():
                 "residues_all_ranks": residues_all,
                 "parallelism": f"dp{world} (sequence shards, no data-path collective"
                                + ("; RCCL all-gather of the scores in every step)" if scaling == "strong" else ")"),
-                "kernel_variant": info["variant"],
+                "kernel_variant": variant,
                 "dequeue_order": "input" if args.no_order else "longest-first",
             },
             "gcups": round(gcups, 2),

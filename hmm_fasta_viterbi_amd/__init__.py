@@ -321,6 +321,10 @@ class MSV_HMM:
         check(_native.lib().msv_profile_describe(self._p, C.byref(info)))
         return info.as_dict()
 
+    def variant_for(self, n: int) -> str:
+        """The kernel variant a batch of n sequences runs (latency / mid / throughput plan)."""
+        return _native.lib().msv_profile_variant_for(self._p, n).decode()
+
     def close(self):
         lib = _loaded_lib()
         if getattr(self, "_p", None) and lib is not None:

@@ -48,7 +48,7 @@ EXPORTED = [
     "msv_fasta_device_max_length", "msv_score_fasta_device", "msv_fasta_device_device",
     "msv_score_batch_async", "msv_profile_wait", "msv_profile_bind_stream",
     "msv_multi_create", "msv_multi_score_batch", "msv_multi_destroy",
-    "msv_host_alloc", "msv_host_free",
+    "msv_host_alloc", "msv_host_free", "msv_profile_variant_for",
 ]
 
 
@@ -134,6 +134,7 @@ def lib() -> C.CDLL:
         "msv_profile_create_from_hmm": (C.c_int, [C.c_int, vp, C.POINTER(vp)]),
         "msv_profile_destroy": (None, [vp]),
         "msv_profile_describe": (C.c_int, [vp, C.POINTER(KernelInfo)]),
+        "msv_profile_variant_for": (C.c_char_p, [vp, C.c_uint64]),
         "msv_profile_reserve_length": (C.c_int, [vp, u64]),
         "msv_score_batch": (C.c_int, [vp, vp, vp, u64, vp, vp]),
         "msv_host_alloc": (C.c_int, [sz, C.POINTER(vp)]),

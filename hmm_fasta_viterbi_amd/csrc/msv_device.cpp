@@ -139,17 +139,21 @@ const msvk::Variant* pick_mid_variant(uint32_t states) {
     return best;
 }
 
-const msvk::Variant* pick_variant(uint32_t states) {
+// `narrow`: 4-lane groups may be picked.  Their rows are long (16 sequences per wave), which the issue
+// model rewards and which wins once the SIMDs are full, so they are the throughput plan of the smallest
+// profiles (100.hmm x 100k: g4_s28 0.339 vs g16_s8 0.521 ms, x 1M 3.08 vs 4.11 ms) while batches that
+// leave the SIMDs part-empty keep a 16-lane plan (x 10k: 0.138 vs 0.099 ms; install_variant).  8-lane
+// groups stay tuning candidates: on 200.hmm g8_s32 against g16_s16 was 6% slower at 100k, 2% faster
+// at 1M (profiles/r02_small_profiles.jsonl).
+const msvk::Variant* pick_variant(uint32_t states, bool narrow) {
     int count = 0;
     const msvk::Variant* all = msvk::variants(&count);
     const msvk::Variant* best = nullptr;
     for (int i = 0; i < count; ++i) {
         const msvk::Variant& v = all[i];
         if (static_cast<uint32_t>(v.G * v.S) < states) continue;
-        // 4/8-lane groups are tuning candidates only: their per-lane rows are longer, which the issue
-        // model rewards, but small profiles are latency-bound and they measured no faster (100.hmm:
-        // g8_s16 0.162 ms, g16_s8 0.165 ms, g4_s28 0.219 ms).
-        if (v.G < 16) continue;
+        // (not for tables of fewer than 80 states: a 28-state lane row would be mostly padding, unmeasured)
+        if (v.G < 16 && !(narrow && v.G == 4 && states >= 80)) continue;
         if (!best || variant_cost(v) < variant_cost(*best)) best = &v;
     }
     return best;
@@ -431,11 +435,16 @@ static msv_status install_mid(msv_profile* p) {
     return MSV_OK;
 }
 
-// Main plan for `v`, and the latency plan (its own table layout) unless it would be the same kernel.
-static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
-    msv_status s = install_plan(p, v, p->main);
+// Main plan for `v`; unless forced, the latency plan (its own table layout) unless it would be the same
+// kernel, and a mid plan (install_mid; or, when the main plan has 4-lane groups, the 16-lane plan for
+// batches that leave the SIMDs part-empty).
+static msv_status install_variant(msv_profile* p, const msvk::Variant* main_v) {
+    msv_status s = install_plan(p, main_v, p->main);
     if (s != MSV_OK) return s;
-    const msvk::Variant* lv = p->force ? nullptr : pick_latency_variant(p->model_length - 1);
+    const uint32_t states = p->model_length - 1;
+    // the 16+-lane plan the latency plan is weighed against (the main plan itself unless it is narrow)
+    const msvk::Variant* v = main_v->G < 16 && !p->force ? pick_variant(states, false) : main_v;
+    const msvk::Variant* lv = p->force ? nullptr : pick_latency_variant(states);
     // Worth it only when the 64-lane row is much shorter than the main row (per-row issue cost,
     // as variant_cost): 1400.hmm 246 vs 96 -> 0.23 vs 0.62 ms at 1024 sequences, 0.37 vs 0.64 at 8192,
     // even at 16384; 1901.hmm 176 vs 123 -> 0.97 vs 1.29 ms at 3 sequences, 1.99 vs 2.89 at 2048;
@@ -445,6 +454,16 @@ static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
     const double ratio = lv ? main_row / lat_row : 0.0;
     drop_plan(p->mid);
     p->mid_max_n = 0;
+    if (v != main_v) {
+        // Narrow main plan: the 16-lane plan while it would not fill the SIMDs -- 3.5 of its waves per
+        // SIMD, where a 16-lane launch turns issue-bound (100.hmm: 14,336 sequences on 256 CUs; the
+        // crossover measured between 10k and 20k, profiles/r02_small_profiles.jsonl).
+        int cus = 0;
+        MSV_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device));
+        s = install_plan(p, v, p->mid);
+        if (s != MSV_OK) return s;
+        p->mid_max_n = static_cast<uint64_t>(3.5 * 4 * cus * (64 / v->G));
+    }
     if (!lv || lv == v || ratio < 1.3) {
         drop_plan(p->lat);
         p->lat_max_n = 0;
@@ -453,6 +472,10 @@ static msv_status install_variant(msv_profile* p, const msvk::Variant* v) {
     p->lat_max_n = static_cast<uint64_t>(std::min(12288.0, 4096.0 * ratio));
     s = install_plan(p, lv, p->lat);
     if (s != MSV_OK) return s;
+    if (p->mid.v) {
+        p->lat_max_n = std::min(p->lat_max_n, p->mid_max_n);
+        return MSV_OK;
+    }
     return install_mid(p);
 }
 
@@ -615,7 +638,7 @@ msv_status msv_profile_create(int device, const float* emission_scores, uint32_t
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MSV_ERR_NO_DEVICE;
     if (device < 0 || device >= ndev) return MSV_ERR_NO_DEVICE;
     const uint32_t R = model_length - 1;  // real match states (MSV_HMM.cpp:285)
-    const msvk::Variant* v = pick_variant(R);
+    const msvk::Variant* v = pick_variant(R, true);
     if (!v) return MSV_ERR_UNSUPPORTED_MODEL;
 
     DeviceGuard g(device);
@@ -765,6 +788,19 @@ msv_status msv_profile_describe(const msv_profile* p, msv_kernel_info* out) {
     return MSV_OK;
 }
 
+// The plan a launch of n sequences takes: latency (n <= lat_max_n), mid (n <= mid_max_n), else main.
+static const Plan& select_plan(const msv_profile* p, uint64_t n, bool latency_ok) {
+    if (!latency_ok) return p->main;
+    if (p->lat.v && n <= p->lat_max_n) return p->lat;
+    if (p->mid.v && n <= p->mid_max_n) return p->mid;
+    return p->main;
+}
+
+const char* msv_profile_variant_for(const msv_profile* p, uint64_t n) {
+    if (!p || !p->main.v) return "";
+    return select_plan(p, n, true).v->name;
+}
+
 // One MSV launch.  `latency_ok`: a batch of few sequences may take the latency plan (not for the
 // pieces of a host pipeline, whose kernels must share the CUs with the next piece's).
 static msv_status launch_batch(msv_profile* p, const uint8_t* d_residues, uint64_t residues_len,
@@ -782,10 +818,7 @@ static msv_status launch_batch(msv_profile* p, const uint8_t* d_residues, uint64
     // Small batches take the latency plan: with fewer sequences than ~4 per SIMD the launch lasts
     // one sequence's rows, and a 64-lane row is far shorter than a 16-lane one.  Mid-size ones (less
     // than one round of the main grid) take the 32-lane plan where there is one (install_variant).
-    const Plan& plan = !latency_ok                            ? p->main
-                       : (p->lat.v && n <= p->lat_max_n)      ? p->lat
-                       : (p->mid.v && n <= p->mid_max_n)      ? p->mid
-                                                              : p->main;
+    const Plan& plan = select_plan(p, n, latency_ok);
     a.etab = plan.d_etab;
     a.residues = residues_len ? d_residues : p->d_dummy;
     a.offsets = d_offsets;

@@ -157,6 +157,9 @@ typedef struct msv_kernel_info {
     uint64_t mid_max_n;        /* batches above latency_max_n, up to this many, take it   */
 } msv_kernel_info;
 msv_status msv_profile_describe(const msv_profile* profile, msv_kernel_info* out);
+/* The kernel variant a batch of n sequences runs (msv_score_batch* / grid launches pick the plan by
+ * batch size: latency plan, mid plan, throughput plan); "" for a null profile. */
+const char* msv_profile_variant_for(const msv_profile* profile, uint64_t n);
 
 /* The compiled kernel family (template instantiations over G, S, waves; names "msv_g<G>_s<S>_w<W>").
  * msv_profile_create picks the cheapest variant with G*S >= LENG; msv_profile_set_variant forces

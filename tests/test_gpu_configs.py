@@ -196,9 +196,18 @@ def test_describe_reports_every_plan():
     # mid-size batches of a large G = 16 profile: the 32-lane plan, above the latency plan's range
     assert d["mid_variant"].startswith("msv_g32_") and d["mid_blocks"] > 0
     assert d["latency_max_n"] < d["mid_max_n"] < d["blocks"] * 64
-    small = msv.MSV_HMM(msv.Profile_HMM(profile_path("100.hmm"))).describe()
+    assert e.variant_for(1) == d["latency_variant"] and e.variant_for(d["latency_max_n"]) == d["latency_variant"]
+    assert e.variant_for(d["latency_max_n"] + 1) == d["mid_variant"] == e.variant_for(d["mid_max_n"])
+    assert e.variant_for(d["mid_max_n"] + 1) == d["variant"] == e.variant_for(10**7)
+    # 100.hmm: 4-lane groups for full batches, the 16-lane plan below 3.5 of its waves per SIMD
+    small_e = msv.MSV_HMM(msv.Profile_HMM(profile_path("100.hmm")))
+    small = small_e.describe()
     assert small["latency_variant"] == "" and small["latency_max_n"] == 0
-    assert small["mid_variant"] == "" and small["mid_max_n"] == 0
+    assert small["variant"].startswith("msv_g4_") and small["mid_variant"].startswith("msv_g16_")
+    assert small_e.variant_for(10_000) == small["mid_variant"] and small_e.variant_for(100_000) == small["variant"]
+    small_e.close()
+    two = msv.MSV_HMM(msv.Profile_HMM(profile_path("200.hmm"))).describe()  # no 4-lane variant covers 200
+    assert two["lanes_per_group"] == 16 and two["mid_variant"] == ""
     g32 = msv.MSV_HMM(msv.Profile_HMM(profile_path("1901.hmm"))).describe()  # main plan already 32 lanes
     assert g32["lanes_per_group"] == 32 and g32["mid_variant"] == ""
     e.close()

@@ -620,7 +620,7 @@ def test_mid_plan_batches_match_main_plan(prof):
     d = auto.describe()
     assert d["mid_variant"].startswith("msv_g32_") and d["latency_max_n"] < d["mid_max_n"]
     n = (d["latency_max_n"] + d["mid_max_n"]) // 2
-    hc, ho = homolog_batch(msv.Profile_HMM(profile_path(prof + ".hmm")).match_emissions, 131, 200, 0, 600)
+    hc, ho = homolog_batch(msv.Profile_HMM(profile_path(prof + ".hmm")).match_emissions, 131, 200, 1, 600)
     codes, offsets = concat_batches(random_batch(130, n - 200, 0, 800), (hc, ho))
     got = auto.score_batch(codes=codes, offsets=offsets)
     forced = msv.MSV_HMM(msv.Profile_HMM(profile_path(prof + ".hmm")))
@@ -628,6 +628,25 @@ def test_mid_plan_batches_match_main_plan(prof):
     assert np.array_equal(bits(got), bits(forced.score_batch(codes=codes, offsets=offsets)))
     sample = np.concatenate([np.arange(0, n, n // 40), np.arange(n - 200, n, 10)])
     assert np.array_equal(bits(got[sample]), bits(OracleProfile(prof).score_batch(*subset(codes, offsets, sample))))
+    auto.close()
+    forced.close()
+
+
+def test_narrow_plan_full_batches_match():
+    """100.hmm: batches that fill the SIMDs run 4-lane groups (16 sequences per wave), smaller ones the
+    16-lane plan; both sizes equal a forced 16-lane launch bitwise, and an oracle sample."""
+    auto = msv.MSV_HMM(msv.Profile_HMM(profile_path("100.hmm")))
+    d = auto.describe()
+    forced = msv.MSV_HMM(msv.Profile_HMM(profile_path("100.hmm")))
+    forced.set_variant(d["mid_variant"])
+    hc, ho = homolog_batch(msv.Profile_HMM(profile_path("100.hmm")).match_emissions, 141, 300, 1, 600)
+    for n in (d["mid_max_n"] - 300, d["mid_max_n"] + 20_000):
+        codes, offsets = concat_batches(random_batch(140 + n, n, 0, 900), (hc, ho))
+        assert auto.variant_for(n + 300) == (d["mid_variant"] if n + 300 <= d["mid_max_n"] else d["variant"])
+        got = auto.score_batch(codes=codes, offsets=offsets)
+        assert np.array_equal(bits(got), bits(forced.score_batch(codes=codes, offsets=offsets))), n
+        sample = np.concatenate([np.arange(0, n, n // 50), np.arange(n, n + 300, 7)])
+        assert np.array_equal(bits(got[sample]), bits(OracleProfile("100").score_batch(*subset(codes, offsets, sample))))
     auto.close()
     forced.close()
 

@@ -63,11 +63,7 @@ def main():
         leng = eng.model_length - 1
         info = eng.describe()
         tcells = residues * leng / (ms * 1e-3) / 1e12
-        # the plan this batch size takes (msv_device.cpp launch_batch)
-        if info["latency_variant"] and n <= info["latency_max_n"]:
-            info["variant"] = info["latency_variant"]
-        elif info["mid_variant"] and n <= info["mid_max_n"]:
-            info["variant"] = info["mid_variant"]
+        info["variant"] = eng.variant_for(n)  # the plan this batch size takes
         print(json.dumps({"config": a.config, "profile": name, "LENG": leng, "n": n, "residues": residues,
                           "variant": info["variant"], "kernel_ms": round(ms, 4),
                           "M_residues_s": round(residues / (ms * 1e-3) / 1e6, 1), "tcells_s": round(tcells, 3),
