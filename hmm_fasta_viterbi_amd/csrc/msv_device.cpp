@@ -231,6 +231,7 @@ struct msv_profile {
     Plan main;                    // throughput plan (every launch unless the batch is small)
     Plan lat;                     // latency plan for small batches (G = 64), may equal main's variant
     Plan mid;                     // mid-size batches (G = 32), large G = 16 profiles only
+    Plan fused;                   // the table in another profile's latency layout (fused grid launches)
     bool force = false;           // msv_profile_set_variant: main plan for every batch size
     uint64_t lat_max_n = 0;       // batches up to this many sequences take the latency plan
     uint64_t mid_max_n = 0;       // batches above lat_max_n and up to this many take the mid plan
@@ -575,6 +576,7 @@ void msv_profile_destroy(msv_profile* p) {
     (void)hipFree(p->main.d_etab);
     (void)hipFree(p->lat.d_etab);
     (void)hipFree(p->mid.d_etab);
+    (void)hipFree(p->fused.d_etab);
     (void)hipFree(p->d_lentab);
     (void)hipFree(p->d_words);
     (void)hipFree(p->d_hist);
@@ -1151,6 +1153,71 @@ msv_status msv_profile_wait(msv_profile* p, uint64_t ticket) {
     return MSV_ERR_INVALID_ARGUMENT;  // unknown ticket, or already waited for
 }
 
+// A grid of few sequences (one 64-lane wave each, at most this many waves over all profiles) runs as ONE
+// launch: every profile's batch takes the latency layout of the grid's largest model, so each
+// profile's launch lasts about as long as it would alone, and all of them run at once instead of
+// queueing on the process's hardware queues (4 by default: 24 profiles x 3 sequences of 3,500
+// residues, benchmark_MSV's shape, took 4.05 ms as 24 launches).
+constexpr uint64_t kFusedMaxSeqs = 2048;
+
+// The plan of `p` whose table is in variant v's layout (installing it as p->fused if none is).
+static msv_status plan_in_layout(msv_profile* p, const msvk::Variant* v, const Plan** out) {
+    for (const Plan* q : {&p->main, &p->lat, &p->mid, &p->fused})
+        if (q->v == v) {
+            *out = q;
+            return MSV_OK;
+        }
+    const msv_status s = install_plan(p, v, p->fused);
+    if (s != MSV_OK) return s;
+    *out = &p->fused;
+    return MSV_OK;
+}
+
+static msv_status grid_fused(msv_profile* const* profiles, uint32_t n_profiles, const msvk::Variant* v,
+                             const uint8_t* d_residues, uint64_t residues_len, const uint64_t* d_offsets, uint64_t n,
+                             const uint32_t* d_order, float* d_scores, hipStream_t cs) {
+    if (residues_len >= (1ull << 32) || !d_offsets || (residues_len && !d_residues)) return MSV_ERR_INVALID_ARGUMENT;
+    const uint32_t groups_per_block = static_cast<uint32_t>(v->waves * (64 / v->G) * v->streams);
+    for (uint32_t first = 0; first < n_profiles; first += msvk::kGridMaxProfiles) {
+        const uint32_t count = std::min(n_profiles - first, msvk::kGridMaxProfiles);
+        msvk::GridArgs ga{};
+        ga.profiles = count;
+        ga.per_profile = static_cast<uint32_t>((n + groups_per_block - 1) / groups_per_block);
+        int slot[msvk::kGridMaxProfiles];
+        for (uint32_t j = 0; j < count; ++j) {
+            msv_profile* p = profiles[first + j];
+            const Plan* plan = nullptr;
+            msv_status s = plan_in_layout(p, v, &plan);
+            if (s != MSV_OK) return s;
+            msvk::KernelArgs& a = ga.p[j];
+            a.etab = plan->d_etab;
+            a.residues = residues_len ? d_residues : p->d_dummy;
+            a.offsets = d_offsets;
+            a.order = d_order;
+            a.lentab = p->d_lentab;
+            a.scores = d_scores + static_cast<uint64_t>(first + j) * n;
+            a.n = n;
+            a.lentab_n = p->lentab_n;
+            a.tr_B_Mk = p->tr_B_Mk;
+            a.tr_E_C = p->tr_E_C;
+            a.tr_E_J = p->tr_E_J;
+            a.stamps = nullptr;
+            MSV_HIP(p->kernels.acquire(cs, &slot[j]));
+            a.counter = p->d_words + 2 * slot[j];
+            a.errors = p->d_words + kErrWord;
+            if (p->kernels.dirty[slot[j]]) MSV_HIP(hipMemsetAsync(a.counter, 0, 2 * sizeof(uint32_t), cs));
+            p->kernels.dirty[slot[j]] = true;
+        }
+        MSV_HIP(msvk::launch_grid_variant(*v, ga, cs));
+        for (uint32_t j = 0; j < count; ++j) {
+            msv_profile* p = profiles[first + j];
+            p->kernels.dirty[slot[j]] = false;
+            MSV_HIP(p->kernels.release(slot[j], cs, lazy_stream(p, cs)));
+        }
+    }
+    return MSV_OK;
+}
+
 msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* d_residues,
                                  uint64_t residues_len, const uint64_t* d_offsets, uint64_t n,
                                  const uint32_t* d_order, float* d_scores, void* stream) {
@@ -1162,6 +1229,17 @@ msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profil
     DeviceGuard g(profiles[0]->device);
     if (!g.ok) return MSV_ERR_NO_DEVICE;
     hipStream_t cs = stream ? static_cast<hipStream_t>(stream) : profiles[0]->stream;
+    if (n_profiles > 1 && n * n_profiles <= kFusedMaxSeqs) {
+        uint32_t states = 0;
+        bool forced = false;
+        for (uint32_t i = 0; i < n_profiles; ++i) {
+            states = std::max(states, profiles[i]->model_length - 1);
+            forced |= profiles[i]->force;  // msv_profile_set_variant: that variant for every batch
+        }
+        const msvk::Variant* fv = forced ? nullptr : pick_latency_variant(states);
+        if (fv && fv->grid_fn)
+            return grid_fused(profiles, n_profiles, fv, d_residues, residues_len, d_offsets, n, d_order, d_scores, cs);
+    }
     hipEvent_t fork = nullptr;
     MSV_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
     struct EventGuard {

@@ -35,6 +35,16 @@ struct KernelArgs {
     uint64_t* stamps;          // diagnostic per-wave timeline (nullptr in production)
 };
 
+// One launch over several profiles (msv_grid_kernel): profile k runs p[k] on workgroups
+// [k * per_profile, (k + 1) * per_profile).  Passed by value (kernarg segment, < 4 KiB).
+constexpr uint32_t kGridMaxProfiles = 32;
+struct GridArgs {
+    uint32_t profiles;
+    uint32_t per_profile;
+    KernelArgs p[kGridMaxProfiles];
+};
+static_assert(sizeof(GridArgs) <= 4096, "kernel arguments are limited to 4 KiB");
+
 struct Variant {
     int G, S, waves, pf, streams;  // pf = emission ring depth; streams = sequences per lane group
     int lds_rows;
@@ -42,6 +52,7 @@ struct Variant {
     const void* fn;
     const char* name;
     int sa = 0;  // split layout: states per lane staged in LDS (0 = whole table layout)
+    const void* grid_fn = nullptr;  // msv_grid_kernel instantiation (G = 64 variants), else nullptr
 };
 
 const Variant* variants(int* count);
@@ -49,6 +60,8 @@ const Variant* variants(int* count);
 // timed launch costs no extra marker packets on the stream.
 hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, hipStream_t stream,
                           hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+// Several profiles in one launch (v.grid_fn must be set).
+hipError_t launch_grid_variant(const Variant& v, const GridArgs& args, hipStream_t stream);
 hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t n, float mu, float lambda,
                           double* pvalues, hipStream_t stream);
 

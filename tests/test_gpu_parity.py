@@ -287,6 +287,24 @@ def test_score_grid_random_fasta_and_seeded():
         assert np.array_equal(bits(grid[k]), bits(engine(prof).score_batch(codes=codes, offsets=offsets))), prof
 
 
+def test_score_grid_fused_launch_matches_per_profile():
+    """A grid of few sequences runs as ONE launch over all profiles (each in the latency layout of the
+    largest model, msv_grid_kernel), in chunks of 32 profiles: 40 entries (all 24 profiles, 16 of them
+    twice) x 50 random + homolog sequences equal every profile's own launch bitwise, and the oracle."""
+    rc, ro = random_batch(150, 40, 0, 900)
+    hc, ho = homolog_batch(msv.Profile_HMM(profile_path("1400.hmm")).match_emissions, 151, 10, 1, 600)
+    codes, offsets = concat_batches((rc, ro), (hc, ho))
+    names = list(PROFILES) + list(PROFILES[:16])
+    engines = [engine(p) for p in names]
+    grid = msv.score_grid(engines, codes=codes, offsets=offsets)
+    assert grid.shape == (40, 50)
+    for k, prof in enumerate(names):
+        assert np.array_equal(bits(grid[k]), bits(engine(prof).score_batch(codes=codes, offsets=offsets))), prof
+    for prof in ("100.hmm", "1400.hmm", "2405.hmm"):
+        want = OracleProfile(prof).score_batch(codes, offsets)
+        assert np.array_equal(bits(grid[names.index(prof)]), bits(want)), prof
+
+
 def test_score_grid_bad_residue_reported_then_cleared():
     """A bad residue in a grid call raises (read from the call's +inf scores, then the profiles' latched
     words are read back and cleared), and the next grid call on good input succeeds bitwise."""
