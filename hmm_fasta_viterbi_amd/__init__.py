@@ -341,11 +341,13 @@ def _handles(engines: Sequence[MSV_HMM]):
 
 
 def score_grid(engines: Sequence[MSV_HMM], seqs: Sequence[str] | None = None, *, codes: np.ndarray | None = None,
-               offsets: np.ndarray | None = None) -> np.ndarray:
+               offsets: np.ndarray | None = None, out: np.ndarray | None = None) -> np.ndarray:
     """Profiles x sequences grid -> float32 [len(engines), n]: the reference's
     benchmark loop over every profile for one FASTA set (benchmark_MSV.cpp:12-24,31-41), as one
-    host call: one upload, one longest-first order, one launch per profile forked onto the
-    profiles' own streams."""
+    host call: one upload, one longest-first order, then ONE fused launch over all profiles for a
+    few sequences, else one launch per profile forked onto the profiles' own streams.  `out`: an
+    optional C-contiguous float32 [len(engines), n] destination (page-locked, e.g. pinned_empty,
+    is written by the kernels directly); page-locked `codes` are read in place."""
     if not engines:
         raise ValueError("score_grid needs at least one profile")
     if seqs is not None:
@@ -353,7 +355,10 @@ def score_grid(engines: Sequence[MSV_HMM], seqs: Sequence[str] | None = None, *,
     codes = np.ascontiguousarray(codes, np.uint8)
     offsets = np.ascontiguousarray(offsets, np.uint64)
     n = len(offsets) - 1
-    out = np.zeros((len(engines), n), np.float32)
+    if out is None:
+        out = np.zeros((len(engines), n), np.float32)
+    elif out.dtype != np.float32 or out.shape != (len(engines), n) or not out.flags.c_contiguous:
+        raise ValueError("out must be a C-contiguous float32 array of shape (len(engines), n)")
     st = _native.lib().msv_score_grid(_handles(engines), len(engines), codes.ctypes.data if codes.size else None,
                                       offsets.ctypes.data, n, out.ctypes.data, None)
     if st == _native.MSV_ERR_BAD_RESIDUE:

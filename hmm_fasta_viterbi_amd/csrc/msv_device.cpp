@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <limits>
+#include <map>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -182,13 +183,21 @@ struct LaunchRing {
             if (e != hipSuccess) return e;
         }
         if (last[k] && last[k] != st) {
-            if (!recorded[k]) {  // lazy: last[k] is a live stream; this covers all of its work so far
-                const hipError_t e = hipEventRecord(done[k], last[k]);
+            // Nothing to wait for when the slot's last launch has completed: its stream is idle, or its
+            // recorded event has fired (host queries, no packets -- a fused grid call acquires a slot
+            // of every profile, and 24 record + wait pairs cost ~0.3 ms before the launch).
+            const bool finished = recorded[k] ? hipEventQuery(done[k]) == hipSuccess
+                                              : hipStreamQuery(last[k]) == hipSuccess;
+            if (!finished) {
+                if (!recorded[k]) {  // lazy: last[k] is a live stream; this covers all of its work so far
+                    const hipError_t e = hipEventRecord(done[k], last[k]);
+                    if (e != hipSuccess) return e;
+                    recorded[k] = true;
+                }
+                const hipError_t e = hipStreamWaitEvent(st, done[k], 0);
                 if (e != hipSuccess) return e;
-                recorded[k] = true;
             }
-            const hipError_t e = hipStreamWaitEvent(st, done[k], 0);
-            if (e != hipSuccess) return e;
+            (void)hipGetLastError();  // a query's hipErrorNotReady is not an error
         }
         *slot = k;
         return hipSuccess;
@@ -288,13 +297,30 @@ struct msv_profile {
     uint64_t* d_stamps = nullptr;  // diagnostic timeline buffer (tools only), or nullptr
     hipEvent_t time_start = nullptr, time_stop = nullptr;  // msv_debug_time_next_launch (one launch)
     hipEvent_t done = nullptr;     // grid API: joins this profile's stream back to the caller's
+    hipStream_t shared = nullptr;  // shared_stream(device) once a host grid call used it
 };
 
 
+// One stream per device that the library never destroys: host grid calls launch on it, so every
+// profile of the grid may leave its slot event unrecorded (a per-profile event record is a packet on
+// the stream: 24 of them put ~115 us between a fused grid launch and its scores' D2H).
+static hipStream_t shared_stream(int device) {
+    static std::mutex mu;
+    static std::map<int, hipStream_t> streams;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = streams.find(device);
+    if (it != streams.end()) return it->second;
+    hipStream_t st = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    streams[device] = st;
+    return st;
+}
+
 // Streams on which a launch may leave its slot event unrecorded (LaunchRing): they stay alive
-// until the profile is destroyed or the binding ends (msv_profile_bind_stream flushes first).
+// until the profile is destroyed or the binding ends (msv_profile_bind_stream flushes first), or
+// forever (shared_stream).
 static bool lazy_stream(const msv_profile* p, hipStream_t st) {
-    return st == p->stream || st == p->stream2 || (p->bound && st == p->bound);
+    return st == p->stream || st == p->stream2 || (p->bound && st == p->bound) || (p->shared && st == p->shared);
 }
 
 // Device address of a page-locked host destination the kernels can write directly (nullptr for
@@ -659,6 +685,14 @@ msv_status msv_profile_create(int device, const float* emission_scores, uint32_t
         msv_profile_destroy(p);
         return hip_status(e);
     }
+    // every launch slot's event up front: created lazily, the first kLaunchSlots launches of a fresh
+    // profile each paid an event creation (~10 us; 24 of them in one fused grid call)
+    for (LaunchRing* ring : {&p->kernels, &p->orders})
+        for (hipEvent_t& ev : ring->done)
+            if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice)) != hipSuccess) {
+                msv_profile_destroy(p);
+                return hip_status(e);
+            }
     if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_words), kWords * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMemset(p->d_words, 0, kWords * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc(reinterpret_cast<void**>(&p->d_dummy), 64)) != hipSuccess ||
@@ -1297,33 +1331,48 @@ msv_status msv_score_grid(msv_profile* const* profiles, uint32_t n_profiles, con
     msv_profile* p0 = profiles[0];
     DeviceGuard g(p0->device);
     if (!g.ok) return MSV_ERR_NO_DEVICE;
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p0->stream;
-    struct Buffers {
-        uint8_t* res = nullptr;
-        uint64_t* off = nullptr;
-        uint32_t* order = nullptr;
-        float* sc = nullptr;
-        ~Buffers() {
-            (void)hipFree(res);
-            (void)hipFree(off);
-            (void)hipFree(order);
-            (void)hipFree(sc);
-        }
-    } b;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : shared_stream(p0->device);
+    if (!st) st = p0->stream;
+    if (!stream)
+        for (uint32_t i = 0; i < n_profiles; ++i) profiles[i]->shared = st;  // lazy slot events (lazy_stream)
+    // The first profile's staging buffers (a host call is synchronous, like msv_score_batch's use of
+    // them): per-call hipMalloc/hipFree of four buffers cost more than the kernels of a small grid.
+    // Page-locked residues are read in place and a page-locked destination is written by the kernels,
+    // as in msv_score_batch.
     const uint64_t total = static_cast<uint64_t>(n_profiles) * n;
-    MSV_HIP(hipMalloc(reinterpret_cast<void**>(&b.res), std::max<uint64_t>(bytes, 1)));
-    MSV_HIP(hipMalloc(reinterpret_cast<void**>(&b.off), (n + 1) * sizeof(uint64_t)));
-    MSV_HIP(hipMalloc(reinterpret_cast<void**>(&b.order), n * sizeof(uint32_t)));
-    MSV_HIP(hipMalloc(reinterpret_cast<void**>(&b.sc), total * sizeof(float)));
-    std::vector<uint64_t> rebased(n + 1);
-    for (uint64_t k = 0; k <= n; ++k) rebased[k] = offsets[k] - offsets[0];
-    if (bytes) MSV_HIP(hipMemcpyAsync(b.res, residues + offsets[0], bytes, hipMemcpyHostToDevice, st));
-    MSV_HIP(hipMemcpyAsync(b.off, rebased.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    msv_status s = msv_order_longest_first(p0, b.off, n, b.order, st);
+    const uint8_t* const zbase = (bytes && p0->zero_copy) ? mapped_host(residues) : nullptr;
+    const uint8_t* const zres = zbase ? zbase + offsets[0] : nullptr;
+    float* const direct = mapped_host(scores);
+    if (!zres) MSV_HIP(ensure(p0->d_res, p0->d_res_cap, std::max<uint64_t>(bytes, 1)));
+    MSV_HIP(ensure(p0->d_off, p0->d_off_cap, n + 1));
+    MSV_HIP(ensure(p0->d_order, p0->d_order_cap, n));
+    if (!direct) MSV_HIP(ensure(p0->d_scores, p0->d_scores_cap, total));
+    if (p0->h_off_cap < n + 8) {  // pinned: the offsets H2D is a true async DMA
+        if (p0->h_off) (void)hipHostFree(p0->h_off);
+        p0->h_off = nullptr;
+        p0->h_off_cap = 0;
+        MSV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p0->h_off), (n + 8) * sizeof(uint64_t), hipHostMallocDefault));
+        p0->h_off_cap = n + 8;
+    }
+    struct Drain {  // an early error return leaves nothing queued that reads h_off or the staging buffers
+        hipStream_t st;
+        bool armed = true;
+        ~Drain() {
+            if (armed) (void)hipStreamSynchronize(st);
+        }
+    } drain{st};
+    for (uint64_t k = 0; k <= n; ++k) p0->h_off[k] = offsets[k] - offsets[0];
+    const uint8_t* d_res = zres ? zres : p0->d_res;
+    if (bytes && !zres) MSV_HIP(hipMemcpyAsync(p0->d_res, residues + offsets[0], bytes, hipMemcpyHostToDevice, st));
+    MSV_HIP(hipMemcpyAsync(p0->d_off, p0->h_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    msv_status s = msv_order_longest_first(p0, p0->d_off, n, p0->d_order, st);
     if (s != MSV_OK) return s;
-    s = msv_score_grid_device(profiles, n_profiles, b.res, std::max<uint64_t>(bytes, 1), b.off, n, b.order, b.sc, st);
+    float* const dsc = direct ? direct : p0->d_scores;
+    s = msv_score_grid_device(profiles, n_profiles, bytes ? d_res : p0->d_dummy, std::max<uint64_t>(bytes, 1),
+                              p0->d_off, n, p0->d_order, dsc, st);
     if (s != MSV_OK) return s;
-    MSV_HIP(hipMemcpyAsync(scores, b.sc, total * sizeof(float), hipMemcpyDeviceToHost, st));
+    if (!direct) MSV_HIP(hipMemcpyAsync(scores, p0->d_scores, total * sizeof(float), hipMemcpyDeviceToHost, st));
+    drain.armed = false;
     MSV_HIP(hipStreamSynchronize(st));  // pageable host buffers above
     // This call's errors show in its scores (+inf: bad residue, NaN: too long), so the profiles' latched
     // error words are read back only when there is one (a 4-byte read-back per profile is a blit kernel

@@ -305,6 +305,22 @@ def test_score_grid_fused_launch_matches_per_profile():
         assert np.array_equal(bits(grid[names.index(prof)]), bits(want)), prof
 
 
+def test_score_grid_pinned_buffers():
+    """Page-locked residues (read in place) and a page-locked destination (written by the kernels),
+    fused (few sequences) and per-profile (many) grid launches: equal to the pageable call."""
+    names = ["100.hmm", "700.hmm", "1400.hmm", "2405.hmm"]
+    engines = [engine(p) for p in names]
+    for n in (40, 3000):
+        codes, offsets = random_batch(160 + n, n, 0, 700)
+        want = msv.score_grid(engines, codes=codes, offsets=offsets)
+        pc = msv.pinned_empty(codes.size, np.uint8)
+        pc[:] = codes
+        out = msv.pinned_empty((len(names), n), np.float32)
+        got = msv.score_grid(engines, codes=pc, offsets=offsets, out=out)
+        assert got is out
+        assert np.array_equal(bits(out), bits(want)), n
+
+
 def test_score_grid_bad_residue_reported_then_cleared():
     """A bad residue in a grid call raises (read from the call's +inf scores, then the profiles' latched
     words are read back and cleared), and the next grid call on good input succeeds bitwise."""

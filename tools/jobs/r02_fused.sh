@@ -8,3 +8,5 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 timeout -k 10 300 python tools/bench_reference_programs.py > $O/refprog.json 2> $O/refprog.err
 GPU_MAX_HW_QUEUES=4 timeout -k 10 300 python tools/bench_reference_programs.py > $O/refprog_q4.json 2> $O/refprog_q4.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rocprof -o run -- python3 tools/bench_reference_programs.py > $O/refprog_rocprof.json 2>&1
+timeout -k 10 300 python bench.py --config cfg2 --no-cpu > $O/bench_cfg2.json 2> $O/bench_cfg2.err
+timeout -k 10 300 python bench.py --no-cpu > $O/bench_cfg3.json 2> $O/bench_cfg3.err
