@@ -438,22 +438,32 @@ static void drop_plan(Plan& plan) {
     plan = Plan{};
 }
 
-// Mid plan (G = 32, two sequences per wave) for the large G = 16 profiles (S >= 64, ~1000-1536
-// states), taken by batches above 1.5 rounds of the latency grid and below 0.9 of one round of the
-// main grid.  There a 16-lane launch runs one partial round of 400-row sequences at ~2-3 waves per
-// SIMD (latency-bound: ~4 ns per instruction per wave), and a 64-lane one needs 2-3 rounds; the
-// 32-lane rows are half as long as the 16-lane ones at twice the waves.  1400.hmm x U[300,500]:
-// 9000 sequences 0.388 ms against 0.458 (latency plan) / 0.527 (main), 12000 0.464 vs 0.536 (main);
-// 1001/1200/1509.hmm alike; at 6000 the latency plan and at 16000 the main plan are as fast or faster
-// (profiles/r02_mid_plans.jsonl).  Smaller profiles measured no consistent gain (500/700.hmm: the
-// 32-lane plan won at some sizes and lost 10-15% at others), so they keep two plans.
+// Mid plan (G = 32, two sequences per wave) for G = 16 profiles with S >= 40 (~600-1536 states), taken
+// by batches between the latency plan's range and about one round of the main grid.  There a 16-lane
+// launch runs one partial round of 400-row sequences at ~2-3 waves per SIMD (latency-bound: ~4 ns per
+// instruction per wave), and a 64-lane one needs 2-3 rounds; the 32-lane rows are half as long as the
+// 16-lane ones at twice the waves.  1400.hmm x U[300,500]: 9000 sequences 0.388 ms against 0.458
+// (latency plan) / 0.527 (main), 12000 0.464 vs 0.536 (main); 600.hmm x 6000 0.151 vs 0.245 (latency)
+// / 0.175 (main); 900.hmm x 9000 0.299 vs 0.353 / 0.367 (profiles/r02_mid_plans.jsonl).
+//  * upper end: 0.9 of one round of the main grid, and for S < 64 at most 10,752 sequences (3/4 of the
+//    16,384 at which 16-lane launches fill 4 waves per SIMD: 800.hmm x 12000 ran 0.326 mid vs 0.291
+//    main, while 1400.hmm x 12000 0.464 vs 0.536);
+//  * lower end (the latency plan's new limit): where the 64-lane row stops being much shorter than the
+//    32-lane one -- 15000 x (mid row / latency row - 1) sequences, within 1.5 rounds of the latency
+//    grid: 1400.hmm (136 vs 96 VALU) ~6,100 (x 6000: 0.302 latency vs 0.306 mid), 600.hmm (76 vs 66)
+//    2,270 (x 6000: mid 38% faster), 800.hmm (96 vs 76) 3,950 (x 6000: mid 8% faster).
+// 500.hmm (S = 32) measured no consistent gain (the 32-lane plan won at some sizes and lost 10-15% at
+// others) and keeps two plans.
 static msv_status install_mid(msv_profile* p) {
     const msvk::Variant* mv = pick_mid_variant(p->model_length - 1);
-    if (!mv || !p->lat.v || p->main.v->G != 16 || p->main.v->S < 64) return MSV_OK;
+    if (!mv || !p->lat.v || p->main.v->G != 16 || p->main.v->S < 40) return MSV_OK;
     const uint64_t lat_cap = static_cast<uint64_t>(p->lat.blocks) * p->lat.groups_per_block;
     const uint64_t main_cap = static_cast<uint64_t>(p->main.blocks) * p->main.groups_per_block;
-    const uint64_t lat_max = std::min<uint64_t>(p->lat_max_n, lat_cap * 3 / 2);
-    const uint64_t mid_max = main_cap * 9 / 10;
+    const double mid_row = 2.5 * mv->S + 26.0;
+    const double lat_row = 2.5 * p->lat.v->S + 36.0 + (p->lat.v->sa ? 2.0 : 0.0);
+    const uint64_t lat_by_rows = static_cast<uint64_t>(std::max(0.0, 15000.0 * (mid_row / lat_row - 1.0)));
+    const uint64_t lat_max = std::min({p->lat_max_n, lat_cap * 3 / 2, lat_by_rows});
+    const uint64_t mid_max = std::min<uint64_t>(main_cap * 9 / 10, p->main.v->S >= 64 ? ~0ull : 10752);
     if (mid_max <= lat_max) return MSV_OK;
     msv_status s = install_plan(p, mv, p->mid);
     if (s != MSV_OK) return s;

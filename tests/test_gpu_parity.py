@@ -645,7 +645,7 @@ def test_latency_plan_small_batches_match_main_plan(prof):
     forced.close()
 
 
-@pytest.mark.parametrize("prof", ["1001", "1400", "1509"])
+@pytest.mark.parametrize("prof", ["600", "900", "1001", "1400", "1509"])
 def test_mid_plan_batches_match_main_plan(prof):
     """Batches between the latency plan's limit and one round of the main grid run the 32-lane mid
     plan (large G = 16 profiles); random and homolog sequences (J >= N rows), empty ones included,
