@@ -146,16 +146,27 @@ const msvk::Variant* pick_mid_variant(uint32_t states) {
 // leave the SIMDs part-empty keep a 16-lane plan (x 10k: 0.138 vs 0.099 ms; install_variant).  8-lane
 // groups stay tuning candidates: on 200.hmm g8_s32 against g16_s16 was 6% slower at 100k, 2% faster
 // at 1M (profiles/r02_small_profiles.jsonl).
-const msvk::Variant* pick_variant(uint32_t states, bool narrow) {
+// A whole-row emission ring (PF = S/4: the next row's chunks requested during this row's epilogue) on
+// 16 waves, for 16-lane rows of 16-32 states.
+static bool whole_row_ring(const msvk::Variant& v) {
+    return v.G == 16 && v.streams == 1 && !v.big && !v.sa && v.pf * 4 == v.S && v.S >= 16 && v.S <= 32;
+}
+
+// `whole_row`: whole-row-ring variants are preferred where they exist -- on full batches 1-5% faster
+// than the PF-2 ones (200/300/400/500.hmm x 100k: 0.692/0.827/1.051/1.196 vs 0.708/0.837/1.094/1.259 ms),
+// while below a round of the grid the PF-2 ones hold (500.hmm x 10k: 0.229 vs 0.197 ms;
+// profiles/r02_whole_row_rings.jsonl), so those stay the plan of smaller batches (install_variant).
+const msvk::Variant* pick_variant(uint32_t states, bool narrow, bool whole_row = false) {
     int count = 0;
     const msvk::Variant* all = msvk::variants(&count);
     const msvk::Variant* best = nullptr;
+    auto cost = [&](const msvk::Variant& v) { return variant_cost(v) * (whole_row && whole_row_ring(v) ? 0.9 : 1.0); };
     for (int i = 0; i < count; ++i) {
         const msvk::Variant& v = all[i];
         if (static_cast<uint32_t>(v.G * v.S) < states) continue;
         // (not for tables of fewer than 80 states: a 28-state lane row would be mostly padding, unmeasured)
         if (v.G < 16 && !(narrow && v.G == 4 && states >= 80)) continue;
-        if (!best || variant_cost(v) < variant_cost(*best)) best = &v;
+        if (!best || cost(v) < cost(*best)) best = &v;
     }
     return best;
 }
@@ -479,8 +490,10 @@ static msv_status install_variant(msv_profile* p, const msvk::Variant* main_v) {
     msv_status s = install_plan(p, main_v, p->main);
     if (s != MSV_OK) return s;
     const uint32_t states = p->model_length - 1;
-    // the 16+-lane plan the latency plan is weighed against (the main plan itself unless it is narrow)
-    const msvk::Variant* v = main_v->G < 16 && !p->force ? pick_variant(states, false) : main_v;
+    // the 16+-lane plan the latency plan is weighed against, and the plan of batches below one round of
+    // the grid: the main plan itself unless it is narrow (4 lanes) or a whole-row-ring variant
+    const msvk::Variant* v =
+        (main_v->G < 16 || whole_row_ring(*main_v)) && !p->force ? pick_variant(states, false) : main_v;
     const msvk::Variant* lv = p->force ? nullptr : pick_latency_variant(states);
     // Worth it only when the 64-lane row is much shorter than the main row (per-row issue cost,
     // as variant_cost): 1400.hmm 246 vs 96 -> 0.23 vs 0.62 ms at 1024 sequences, 0.37 vs 0.64 at 8192,
@@ -494,12 +507,14 @@ static msv_status install_variant(msv_profile* p, const msvk::Variant* main_v) {
     if (v != main_v) {
         // Narrow main plan: the 16-lane plan while it would not fill the SIMDs -- 3.5 of its waves per
         // SIMD, where a 16-lane launch turns issue-bound (100.hmm: 14,336 sequences on 256 CUs; the
-        // crossover measured between 10k and 20k, profiles/r02_small_profiles.jsonl).
+        // crossover measured between 10k and 20k, profiles/r02_small_profiles.jsonl).  Whole-row-ring
+        // main plan: the PF-2 variant up to 3/4 of that (10,752).
         int cus = 0;
         MSV_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device));
         s = install_plan(p, v, p->mid);
         if (s != MSV_OK) return s;
-        p->mid_max_n = static_cast<uint64_t>(3.5 * 4 * cus * (64 / v->G));
+        const double fill = main_v->G < 16 ? 3.5 : 2.625;
+        p->mid_max_n = static_cast<uint64_t>(fill * 4 * cus * (64 / v->G));
     }
     if (!lv || lv == v || ratio < 1.3) {
         drop_plan(p->lat);
@@ -676,7 +691,7 @@ msv_status msv_profile_create(int device, const float* emission_scores, uint32_t
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MSV_ERR_NO_DEVICE;
     if (device < 0 || device >= ndev) return MSV_ERR_NO_DEVICE;
     const uint32_t R = model_length - 1;  // real match states (MSV_HMM.cpp:285)
-    const msvk::Variant* v = pick_variant(R, true);
+    const msvk::Variant* v = pick_variant(R, true, true);
     if (!v) return MSV_ERR_UNSUPPORTED_MODEL;
 
     DeviceGuard g(device);

@@ -206,8 +206,12 @@ def test_describe_reports_every_plan():
     assert small["variant"].startswith("msv_g4_") and small["mid_variant"].startswith("msv_g16_")
     assert small_e.variant_for(10_000) == small["mid_variant"] and small_e.variant_for(100_000) == small["variant"]
     small_e.close()
-    two = msv.MSV_HMM(msv.Profile_HMM(profile_path("200.hmm"))).describe()  # no 4-lane variant covers 200
-    assert two["lanes_per_group"] == 16 and two["mid_variant"] == ""
+    # 200.hmm: a whole-row-ring variant for full batches, the PF-2 one below 10,752 sequences
+    two_e = msv.MSV_HMM(msv.Profile_HMM(profile_path("200.hmm")))
+    two = two_e.describe()
+    assert two["variant"] == "msv_g16_s16_w16_p4_d1" and two["mid_variant"] == "msv_g16_s16_w8_p2_d1"
+    assert two_e.variant_for(10_000) == two["mid_variant"] and two_e.variant_for(20_000) == two["variant"]
+    two_e.close()
     g32 = msv.MSV_HMM(msv.Profile_HMM(profile_path("1901.hmm"))).describe()  # main plan already 32 lanes
     assert g32["lanes_per_group"] == 32 and g32["mid_variant"] == ""
     e.close()

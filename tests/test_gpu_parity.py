@@ -685,6 +685,26 @@ def test_narrow_plan_full_batches_match():
     forced.close()
 
 
+@pytest.mark.parametrize("prof", ["200", "400", "500"])
+def test_whole_row_ring_plan_matches(prof):
+    """200-500-state profiles: full batches run a whole-row-ring variant, smaller ones the PF-2 variant;
+    both sizes equal a forced PF-2 launch bitwise, and an oracle sample."""
+    auto = msv.MSV_HMM(msv.Profile_HMM(profile_path(prof + ".hmm")))
+    d = auto.describe()
+    assert d["variant"] != d["mid_variant"] and d["mid_max_n"] > 0
+    forced = msv.MSV_HMM(msv.Profile_HMM(profile_path(prof + ".hmm")))
+    forced.set_variant(d["mid_variant"])
+    hc, ho = homolog_batch(msv.Profile_HMM(profile_path(prof + ".hmm")).match_emissions, 171, 200, 1, 600)
+    for n in (d["mid_max_n"] - 200, d["mid_max_n"] + 10_000):
+        codes, offsets = concat_batches(random_batch(170 + n, n, 0, 900), (hc, ho))
+        got = auto.score_batch(codes=codes, offsets=offsets)
+        assert np.array_equal(bits(got), bits(forced.score_batch(codes=codes, offsets=offsets))), n
+        sample = np.concatenate([np.arange(0, n, n // 40), np.arange(n, n + 200, 9)])
+        assert np.array_equal(bits(got[sample]), bits(OracleProfile(prof).score_batch(*subset(codes, offsets, sample))))
+    auto.close()
+    forced.close()
+
+
 def test_score_batch_multi_concurrent_length_table_growth():
     """Each shard holds a sequence longer than the default length table, so every host thread of
     msv_score_batch_multi grows its profile's table at once (shared host cache under a lock)."""

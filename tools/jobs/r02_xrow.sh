@@ -1,6 +1,16 @@
+# Whole-row emission rings (cross-row prefetch, PF = S/4, 16 waves) against the PF-2 throughput variants
+# for 200-500-state profiles at 10k and 100k sequences.
 set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r02_xrow
 mkdir -p $O
-timeout -k 10 400 python tools/kernel_ab.py --config cfg2 --rounds 4 ab/new/libmsv_hip.so ab/xrow2/libmsv_hip.so > $O/kab_cfg2.jsonl 2> $O/kab_cfg2.err
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 240 --timeout-method thread > $O/pytest_parity.log 2>&1
-timeout -k 10 300 python bench.py --no-cpu > $O/bench_cfg3.json 2> $O/bench_cfg3.err
+run() {
+  for n in 10000 100000; do
+    echo "{\"profile\": \"$1\", \"n\": $n}" >> $O/tune_xrow.jsonl
+    timeout -k 10 200 python tools/tune.py --profile $1 --n $n --rounds 2 --variants $2 >> $O/tune_xrow.jsonl
+  done
+}
+run 200.hmm msv_g16_s16_w8_p2_d1,msv_g16_s16_w16_p4_d1
+run 300.hmm msv_g16_s20_w8_p2_d1,msv_g16_s20_w16_p5_d1
+run 400.hmm msv_g16_s28_w8_p2_d1,msv_g16_s28_w16_p7_d1
+run 500.hmm msv_g16_s32_w12_p2_d1,msv_g16_s32_w16_p8_d1
