@@ -305,6 +305,23 @@ def test_score_grid_fused_launch_matches_per_profile():
         assert np.array_equal(bits(grid[names.index(prof)]), bits(want)), prof
 
 
+@pytest.mark.parametrize("leng", [2600, 3500])
+def test_score_grid_fused_big_layout(tmp_path, leng):
+    """The fused grid launch in the latency layout of a model too large for LDS (split 64-lane layout at
+    2600 states, BIG row-class layout at 3500), shared by small profiles: equal to per-profile launches."""
+    from hmm_fasta_viterbi_amd.synthetic import write_hmm
+    path = str(tmp_path / f"syn{leng}.hmm")
+    write_hmm(path, leng, leng)
+    big = msv.MSV_HMM(msv.Profile_HMM(path))
+    engines = [big, engine("100.hmm"), engine("1400.hmm"), engine("2405.hmm")]
+    codes, offsets = random_batch(190 + leng, 30, 0, 800)
+    grid = msv.score_grid(engines, codes=codes, offsets=offsets)
+    for k, e in enumerate(engines):
+        assert np.array_equal(bits(grid[k]), bits(e.score_batch(codes=codes, offsets=offsets))), k
+    assert np.array_equal(bits(grid[0]), bits(OracleProfile(path).score_batch(codes, offsets)))
+    big.close()
+
+
 def test_score_grid_pinned_buffers():
     """Page-locked residues (read in place) and a page-locked destination (written by the kernels),
     fused (few sequences) and per-profile (many) grid launches: equal to the pageable call."""
