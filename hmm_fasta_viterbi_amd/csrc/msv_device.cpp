@@ -866,7 +866,8 @@ const char* msv_profile_variant_for(const msv_profile* p, uint64_t n) {
 // pieces of a host pipeline, whose kernels must share the CUs with the next piece's).
 static msv_status launch_batch(msv_profile* p, const uint8_t* d_residues, uint64_t residues_len,
                                const uint64_t* d_offsets, uint64_t n, const uint32_t* d_order, float* d_scores,
-                               void* stream, bool latency_ok, uint32_t* d_errors = nullptr) {
+                               void* stream, bool latency_ok, uint32_t* d_errors = nullptr,
+                               bool host_residues = false) {
     if (!p) return MSV_ERR_INVALID_ARGUMENT;
     if (n == 0) return MSV_OK;
     if (!d_offsets || !d_scores || (residues_len && !d_residues)) return MSV_ERR_INVALID_ARGUMENT;
@@ -906,7 +907,7 @@ static msv_status launch_batch(msv_profile* p, const uint8_t* d_residues, uint64
     p->kernels.dirty[k] = true;
     hipEvent_t t0 = p->time_start, t1 = p->time_stop;
     p->time_start = p->time_stop = nullptr;
-    MSV_HIP(msvk::launch_variant(*plan.v, dim3(blocks), a, st, t0, t1));
+    MSV_HIP(msvk::launch_variant(*plan.v, dim3(blocks), a, st, t0, t1, host_residues));
     p->kernels.dirty[k] = false;
     MSV_HIP(p->kernels.release(k, st, lazy_stream(p, st)));
     return MSV_OK;
@@ -916,6 +917,14 @@ msv_status msv_score_batch_device(msv_profile* p, const uint8_t* d_residues, uin
                                   const uint64_t* d_offsets, uint64_t n, const uint32_t* d_order, float* d_scores,
                                   void* stream) {
     return launch_batch(p, d_residues, residues_len, d_offsets, n, d_order, d_scores, stream, true);
+}
+
+// Library-internal (msv_multi.cpp): msv_score_batch_device for residues that are the device alias of
+// page-locked host memory -- the launch takes the variant's zero-copy twin (msv_kernel.hip zc_fn).
+__attribute__((visibility("hidden"))) msv_status msv_score_batch_host_residues(
+    msv_profile* p, const uint8_t* d_residues, uint64_t residues_len, const uint64_t* d_offsets, uint64_t n,
+    const uint32_t* d_order, float* d_scores, void* stream) {
+    return launch_batch(p, d_residues, residues_len, d_offsets, n, d_order, d_scores, stream, true, nullptr, true);
 }
 
 msv_status msv_profile_bind_stream(msv_profile* p, void* stream) {
@@ -1099,7 +1108,7 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         if (pipe) MSV_HIP(hipStreamWaitEvent(c, p->events[2 + k], 0));
         const uint8_t* src = zres ? zres + base0 + lo : p->d_res + lo;
         s = launch_batch(p, bytes ? src : p->d_dummy, std::max<uint64_t>(bytes, 1), p->d_off + cut[k] + k,
-                         cut[k + 1] - cut[k], p->d_order + cut[k], dsc + cut[k], c, !pipe);
+                         cut[k + 1] - cut[k], p->d_order + cut[k], dsc + cut[k], c, !pipe, nullptr, zres && bytes);
         if (s != MSV_OK) return s;
     }
     if (pipe) {  // join the second compute stream (done before the last piece) back into the caller's

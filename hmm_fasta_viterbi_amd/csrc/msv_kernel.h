@@ -53,13 +53,16 @@ struct Variant {
     const char* name;
     int sa = 0;  // split layout: states per lane staged in LDS (0 = whole table layout)
     const void* grid_fn = nullptr;  // msv_grid_kernel instantiation (G = 64 variants), else nullptr
+    const void* zc_fn = nullptr;    // zero-copy twin (residues two rows ahead), else nullptr
 };
 
 const Variant* variants(int* count);
 // start/stop (optional): events updated with the kernel's own start and end (hipExtLaunchKernel), so a
 // timed launch costs no extra marker packets on the stream.
+// host_residues: args.residues is the device alias of page-locked host memory (the zero-copy twin
+// runs when the variant has one).
 hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, hipStream_t stream,
-                          hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+                          hipEvent_t start = nullptr, hipEvent_t stop = nullptr, bool host_residues = false);
 // Several profiles in one launch (v.grid_fn must be set).
 hipError_t launch_grid_variant(const Variant& v, const GridArgs& args, hipStream_t stream);
 hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t n, float mu, float lambda,

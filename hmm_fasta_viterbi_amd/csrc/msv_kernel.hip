@@ -193,7 +193,8 @@ struct RowCtx {
 // LDS, its last S - SA states (the "B block") are read from the global table (L2) for every row -- no
 // per-row LDS/L2 class branch, so the groups of a wave run the same row body whatever their residues;
 // the next row's B halves are requested one row ahead.
-template <int G, int S, int WAVES, int PF, bool BIG, int D, int SA = 0>
+// RPFO > 0 overrides the rows of residue prefetch (the zero-copy twins below).
+template <int G, int S, int WAVES, int PF, bool BIG, int D, int SA = 0, int RPFO = 0>
 __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs a) {
 #define MSV_BLOCK blockIdx.x
 #define MSV_BLOCKS gridDim.x
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(WAVES * 64) void msv_batch_kernel(const KernelArgs 
 // table in this variant's layout, its counter slot, scores and specials -- exactly as msv_batch_kernel
 // would with a grid of per_profile workgroups.  The arguments travel in the kernarg segment (copied
 // at launch: nothing for the host to keep alive).
-template <int G, int S, int WAVES, int PF, bool BIG, int D, int SA = 0>
+template <int G, int S, int WAVES, int PF, bool BIG, int D, int SA = 0, int RPFO = 0>
 __global__ __launch_bounds__(WAVES * 64) void msv_grid_kernel(const GridArgs g) {
     const uint32_t profile = blockIdx.x / g.per_profile;
     const uint32_t per_profile = g.per_profile;
@@ -226,6 +227,19 @@ __global__ __launch_bounds__(WAVES * 64) void msv_grid_kernel(const GridArgs g) 
 template <int G, int S, int WAVES, int PF, bool BIG, int D, int SA = 0>
 constexpr const void* grid_fn() {
     if constexpr (G == 64 && D == 1) return reinterpret_cast<const void*>(&msv_grid_kernel<G, S, WAVES, PF, BIG, D, SA>);
+    else return nullptr;
+}
+
+// Zero-copy twins: the same variant reading its residues two rows ahead -- which for 16/32-lane rows
+// means residue BLOCKS (one byte load per lane per 16 rows, a block ahead) -- for launches whose
+// residues sit in page-locked host memory.  A row of 41-96 states is long enough that one row of
+// prefetch hides an HBM/L2 load, not a PCIe round trip at each 128-B line: cfg3 read in place 2.945 vs
+// 2.856 ms with the twin, while from HBM it is 0.3-0.7% slower on 1400/1901.hmm (2% faster on
+// 1001.hmm) -- profiles/r02_zero_copy_twins.jsonl.  Split variants already prefetch two rows.
+template <int G, int S, int WAVES, int PF, bool BIG, int D, int SA = 0>
+constexpr const void* zc_fn() {
+    if constexpr ((G == 16 || G == 32) && D == 1 && !BIG && SA == 0 && S > 40)
+        return reinterpret_cast<const void*>(&msv_batch_kernel<G, S, WAVES, PF, BIG, D, SA, 2>);
     else return nullptr;
 }
 
@@ -346,7 +360,8 @@ hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t
             reinterpret_cast<const void*>(                                                                 \
                 &msv_batch_kernel<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_>),               \
             "msv_g" #G_ "_s" #S_ "_w" #W_ "_p" #P_ "_d" #D_, 0,                                              \
-            grid_fn<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_>()}
+            grid_fn<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_>(),                            \
+            zc_fn<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_>()}
 
 // Split layout (G = 32 or 64): SA states per lane from LDS (20 rows), S - SA from L2.
 #define MSV_SPLIT_VARIANT(G_, S_, SA_, W_, P_)                                                            \
@@ -364,10 +379,11 @@ const Variant* variants(int* count) {
 }
 
 hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, hipStream_t stream, hipEvent_t start,
-                          hipEvent_t stop) {
+                          hipEvent_t stop, bool host_residues) {
     void* params[] = {const_cast<KernelArgs*>(&args)};
-    if (start || stop) return hipExtLaunchKernel(v.fn, grid, dim3(v.waves * 64), params, 0, stream, start, stop, 0);
-    return hipLaunchKernel(v.fn, grid, dim3(v.waves * 64), params, 0, stream);
+    const void* fn = host_residues && v.zc_fn ? v.zc_fn : v.fn;
+    if (start || stop) return hipExtLaunchKernel(fn, grid, dim3(v.waves * 64), params, 0, stream, start, stop, 0);
+    return hipLaunchKernel(fn, grid, dim3(v.waves * 64), params, 0, stream);
 }
 
 hipError_t launch_grid_variant(const Variant& v, const GridArgs& args, hipStream_t stream) {

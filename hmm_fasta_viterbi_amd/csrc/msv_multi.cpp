@@ -19,6 +19,11 @@
 
 #include "msv.h"
 
+// msv_device.cpp (library-internal): msv_score_batch_device for page-locked host residues (zero-copy twin).
+extern "C" msv_status msv_score_batch_host_residues(msv_profile* p, const uint8_t* d_residues, uint64_t residues_len,
+                                         const uint64_t* d_offsets, uint64_t n, const uint32_t* d_order,
+                                         float* d_scores, void* stream);
+
 namespace {
 
 constexpr uint64_t kChunkBytes = (1ull << 32) - (1ull << 20);  // per launch (msv_score_batch_device)
@@ -135,8 +140,8 @@ msv_status enqueue_shard(Rank& r, const uint8_t* residues, const uint64_t* offse
             MM_HIP(grow(r.d_res, r.res_cap, 1));
             src = r.d_res;
         }
-        s = msv_score_batch_device(r.profile, src, std::max<uint64_t>(bytes, 1), r.d_off, n, r.d_ord,
-                                   r.d_sc + (a - first), r.stream);
+        s = (zres && bytes ? msv_score_batch_host_residues : msv_score_batch_device)(
+            r.profile, src, std::max<uint64_t>(bytes, 1), r.d_off, n, r.d_ord, r.d_sc + (a - first), r.stream);
         if (s != MSV_OK) return s;
         // h_off (pageable) is rewritten by the next chunk: let this chunk's copy finish first
         if (b < last) MM_HIP(hipStreamSynchronize(r.stream));

@@ -295,6 +295,26 @@ def test_pinned_destinations_written_by_kernel():
     e.close()
 
 
+@pytest.mark.parametrize("prof", ["700", "1600", "1901"])
+def test_zero_copy_twin_variants(prof):
+    """Page-locked residues of a full batch run the variant's zero-copy twin (residue blocks instead of
+    one row of prefetch, msv_kernel.hip zc_fn): random + homolog sequences equal a device launch of the
+    ordinary variant bitwise, and the oracle on a sample."""
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path(prof + ".hmm")))
+    assert e.describe()["states_per_lane"] > 40
+    hc, ho = homolog_batch(msv.Profile_HMM(profile_path(prof + ".hmm")).match_emissions, 531, 300, 1, 700)
+    codes, offsets = concat_batches(random_batch(530, 24_000, 0, 800), (hc, ho))
+    want = device_scores(e, codes, offsets)
+    pc = msv.pinned_empty(codes.size, np.uint8)
+    pc[:] = codes
+    got = e.score_batch(codes=pc, offsets=offsets)
+    assert np.array_equal(bits(got), bits(want))
+    n = len(offsets) - 1
+    sample = np.concatenate([np.arange(0, n - 300, 997), np.arange(n - 300, n, 11)])
+    assert np.array_equal(bits(got[sample]), bits(OracleProfile(prof).score_batch(*subset(codes, offsets, sample))))
+    e.close()
+
+
 def test_zero_copy_pinned_residues():
     """Page-locked residues are read by the kernel in place (no H2D): bitwise equal to the copy
     pipeline (zero-copy switched off) and to a device launch -- for a > 4 Mi-residue batch (one launch
