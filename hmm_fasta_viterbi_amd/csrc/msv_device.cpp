@@ -964,14 +964,16 @@ msv_status msv_order_longest_first(msv_profile* p, const uint64_t* d_offsets, ui
     if (!g.ok) return MSV_ERR_NO_DEVICE;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p->stream;
     if (!p->d_hist) {
-        MSV_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_hist), kLaunchSlots * 2 * kOrderBins * sizeof(uint32_t)));
+        MSV_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_hist),
+                            kLaunchSlots * msvk::kOrderScratchWords(kOrderBins) * sizeof(uint32_t)));
         p->hist_dirty.fill(true);
     }
     int k = 0;
     MSV_HIP(p->orders.acquire(st, &k));
-    // [histogram | cursors] per slot; the sort leaves its histogram zeroed for the slot's next use
-    uint32_t* scratch = p->d_hist + static_cast<size_t>(k) * 2 * kOrderBins;
-    if (p->hist_dirty[k]) MSV_HIP(hipMemsetAsync(scratch, 0, kOrderBins * sizeof(uint32_t), st));
+    // [histogram | cursors | ticket] per slot; the sort leaves histogram and ticket zeroed for the slot's next use
+    uint32_t* scratch = p->d_hist + static_cast<size_t>(k) * msvk::kOrderScratchWords(kOrderBins);
+    if (p->hist_dirty[k])
+        MSV_HIP(hipMemsetAsync(scratch, 0, msvk::kOrderScratchWords(kOrderBins) * sizeof(uint32_t), st));
     p->hist_dirty[k] = true;
     MSV_HIP(msvk::launch_order(d_offsets, n, scratch, kOrderBins, d_order, st));
     p->hist_dirty[k] = false;

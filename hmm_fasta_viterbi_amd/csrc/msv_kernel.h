@@ -68,8 +68,10 @@ hipError_t launch_grid_variant(const Variant& v, const GridArgs& args, hipStream
 hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t n, float mu, float lambda,
                           double* pvalues, hipStream_t stream);
 
-// scratch_hist: 2 * nbins words [histogram | cursors]; the histogram must be zero on entry and is
-// zero again when the sort completes (zero it once when fresh, or after a failed launch).
+// scratch_hist: kOrderScratchWords(nbins) words [histogram | cursors | ticket]; histogram and ticket must
+// be zero on entry and are zero again when the sort completes (zero them once when fresh, or after a
+// failed launch).  1024 <= nbins <= 4096 (the scan runs 1024 threads over 4 bins each).
+constexpr uint32_t kOrderScratchWords(uint32_t nbins) { return 2 * nbins + 64; }
 hipError_t launch_order(const uint64_t* offsets, uint64_t n, uint32_t* scratch_hist, uint32_t nbins, uint32_t* order,
                         hipStream_t stream);
 

@@ -245,11 +245,12 @@ constexpr const void* zc_fn() {
 
 // ------------------------------------------------------------------------------------------------
 // Longest-first dequeue order: a device counting sort on sequence length (lengths >= nbins-1 share
-// the first bin).  Three small launches, histograms privatised in LDS so global atomics are one
-// per (block, non-empty bin):  count -> scan -> place.  Order inside a bin is arbitrary (it never
-// changes a score: every score is written to its own sequence's slot).  The scratch is [hist |
-// cursor]: the scan writes the cursors and zeroes the histogram for the next sort, so no memset
-// launch precedes a sort (the caller zeroes a fresh or failed scratch once).
+// the first bin).  Two small launches, histograms privatised in LDS so global atomics are one
+// per (block, non-empty bin):  count (+ scan by the last block to finish) -> place.  Order inside a
+// bin is arbitrary (it never changes a score: every score is written to its own sequence's slot).
+// The scratch is [hist | cursor | ticket]: the scan writes the cursors and zeroes the histogram and
+// the ticket for the next sort, so no memset launch precedes a sort (the caller zeroes a fresh or
+// failed scratch once).  (A separate one-block scan launch cost ~5 us of launch latency per sort.)
 // ------------------------------------------------------------------------------------------------
 constexpr int kOrderThreads = 1024;
 
@@ -258,10 +259,68 @@ __device__ __forceinline__ uint32_t length_bin(const uint64_t* __restrict__ offs
     return nbins - 1 - static_cast<uint32_t>(L >= nbins - 1 ? nbins - 1 : L);  // descending length
 }
 
+// Exclusive prefix sum of one value per thread over the block (kOrderThreads threads): a shuffle scan
+// inside each wave, the 16 wave totals scanned by wave 0, two barriers (a Hillis-Steele scan over the
+// block took 10 steps of two barriers each, ~5 us of a sort).  part: >= 16 words of LDS.
+__device__ __forceinline__ uint32_t block_exclusive_sum(uint32_t v, uint32_t* part) {
+    constexpr uint32_t kWaves = kOrderThreads / 64;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= static_cast<uint32_t>(d)) x += y;
+    }
+    if (lane == 63) part[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        uint32_t t = lane < kWaves ? part[lane] : 0u;
+#pragma unroll
+        for (int d = 1; d < static_cast<int>(kWaves); d <<= 1) {
+            const uint32_t y = __shfl_up(t, d, 64);
+            if (lane >= static_cast<uint32_t>(d)) t += y;
+        }
+        if (lane < kWaves) part[lane] = t;
+    }
+    __syncthreads();
+    return (w ? part[w - 1] : 0u) + x - v;
+}
+
+// Exclusive scan of hist[nbins] into cursor[nbins], hist zeroed (one block, nbins <= 4 * kOrderThreads;
+// part: 16 words of LDS).  hist is read with device-scope loads: the other blocks' counts
+// arrived by atomics at L2.
+__device__ __forceinline__ void scan_bins(uint32_t* __restrict__ hist, uint32_t* __restrict__ cursor, uint32_t nbins,
+                                          uint32_t* part) {
+    const uint32_t t = threadIdx.x;
+    uint32_t v[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = 4 * t + q;
+        v[q] = i < nbins ? __hip_atomic_load(&hist[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        if (i < nbins) hist[i] = 0u;
+        sum += v[q];
+    }
+    uint32_t run = block_exclusive_sum(sum, part);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = 4 * t + q;
+        if (i < nbins) cursor[i] = run;
+        run += v[q];
+    }
+}
+
+// scratch = [hist | cursor | ticket]; the last block to add its counts runs the scan, and no block
+// waits for another.  The hand-off needs no fences: the counts are agent-scope atomics (performed past
+// the XCD's L2), every wave drains them (vmcnt) before the block's ticket add, and the block whose add
+// returns the last ticket reads them with sc1 loads after a barrier (MI355X_MICROARCH.md,
+// inter-workgroup visibility, first row of the sc1 hand-offs).  A __threadfence() in every block
+// (L2 write-back + invalidate) made this launch 57 us instead of 5.
 __global__ __launch_bounds__(kOrderThreads) void order_count_kernel(const uint64_t* __restrict__ offsets, uint64_t n,
-                                                                    uint64_t chunk, uint32_t* __restrict__ hist,
+                                                                    uint64_t chunk, uint32_t* __restrict__ scratch,
                                                                     uint32_t nbins) {
-    extern __shared__ uint32_t lh[];
+    extern __shared__ uint32_t lh[];  // nbins words: block counts, then the scan partials (last block)
+    __shared__ uint32_t ticket;
+    uint32_t* const hist = scratch;
     for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x) lh[i] = 0;
     __syncthreads();
     const uint64_t lo = blockIdx.x * chunk, hi = min(n, lo + chunk);
@@ -269,36 +328,13 @@ __global__ __launch_bounds__(kOrderThreads) void order_count_kernel(const uint64
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x)
         if (lh[i]) atomicAdd(&hist[i], lh[i]);
-}
-
-// Exclusive scan of hist[nbins] into cursor[nbins], hist zeroed (one block; nbins <= 4 * kOrderThreads).
-__global__ __launch_bounds__(kOrderThreads) void order_scan_kernel(uint32_t* __restrict__ hist,
-                                                                   uint32_t* __restrict__ cursor, uint32_t nbins) {
-    __shared__ uint32_t part[kOrderThreads];
-    const uint32_t t = threadIdx.x;
-    uint32_t v[4], sum = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t i = 4 * t + q;
-        v[q] = i < nbins ? hist[i] : 0u;
-        if (i < nbins) hist[i] = 0u;
-        sum += v[q];
-    }
-    part[t] = sum;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's count atomics have completed
     __syncthreads();
-    for (uint32_t d = 1; d < kOrderThreads; d <<= 1) {  // Hillis-Steele inclusive scan
-        const uint32_t x = t >= d ? part[t - d] : 0u;
-        __syncthreads();
-        part[t] += x;
-        __syncthreads();
-    }
-    uint32_t run = part[t] - sum;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t i = 4 * t + q;
-        if (i < nbins) cursor[i] = run;
-        run += v[q];
-    }
+    if (threadIdx.x == 0) ticket = atomicAdd(scratch + 2 * nbins, 1u);
+    __syncthreads();
+    if (ticket != gridDim.x - 1) return;
+    scan_bins(hist, scratch + nbins, nbins, lh);
+    if (threadIdx.x == 0) scratch[2 * nbins] = 0u;
 }
 
 __global__ __launch_bounds__(kOrderThreads) void order_place_kernel(const uint64_t* __restrict__ offsets, uint64_t n,
@@ -415,7 +451,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_small_kernel(const uint64
     for (int k = 0; k < kSmallOrderPer; ++k)
         if (bin[k] != 0xFFFFFFFFu) atomicAdd(&lh[bin[k]], 1u);
     __syncthreads();
-    // exclusive scan of lh[0..nbins): 4 consecutive bins per thread, Hillis-Steele over threads
+    // exclusive scan of lh[0..nbins): 4 consecutive bins per thread, block_exclusive_sum over threads
     uint32_t v[4], sum = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -423,15 +459,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_small_kernel(const uint64
         v[q] = i < nbins ? lh[i] : 0u;
         sum += v[q];
     }
-    part[t] = sum;
-    __syncthreads();
-    for (uint32_t d = 1; d < kOrderThreads; d <<= 1) {
-        const uint32_t x = t >= d ? part[t - d] : 0u;
-        __syncthreads();
-        part[t] += x;
-        __syncthreads();
-    }
-    uint32_t run = part[t] - sum;
+    uint32_t run = block_exclusive_sum(sum, part);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint32_t i = 4 * t + q;
@@ -446,7 +474,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_small_kernel(const uint64
 
 hipError_t launch_order(const uint64_t* offsets, uint64_t n, uint32_t* scratch_hist, uint32_t nbins, uint32_t* order,
                         hipStream_t stream) {
-    if (nbins > 4 * kOrderThreads) return hipErrorInvalidValue;
+    if (nbins > 4 * kOrderThreads || nbins < kOrderThreads) return hipErrorInvalidValue;
     if (n <= static_cast<uint64_t>(kSmallOrderPer) * kOrderThreads) {
         const size_t lds = (nbins + kOrderThreads) * sizeof(uint32_t);
         hipLaunchKernelGGL(order_small_kernel, dim3(1), dim3(kOrderThreads), lds, stream, offsets,
@@ -458,8 +486,6 @@ hipError_t launch_order(const uint64_t* offsets, uint64_t n, uint32_t* scratch_h
     const size_t lds = nbins * sizeof(uint32_t);
     hipLaunchKernelGGL(order_count_kernel, dim3(blocks), dim3(kOrderThreads), lds, stream, offsets, n, chunk,
                        scratch_hist, nbins);
-    hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(kOrderThreads), 0, stream, scratch_hist,
-                       scratch_hist + nbins, nbins);
     hipLaunchKernelGGL(order_place_kernel, dim3(blocks), dim3(kOrderThreads), lds, stream, offsets, n, chunk,
                        scratch_hist + nbins, nbins, order);
     return hipGetLastError();

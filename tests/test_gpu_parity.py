@@ -416,8 +416,9 @@ def test_pvalues_device_matches_host():
 
 @pytest.mark.parametrize("n", [1, 1000, 16384, 16385, 200_000])
 def test_order_longest_first_sizes(n):
-    """Both order paths (one-launch small sort up to 16384, three-launch sort above) give a
-    permutation in non-increasing length order (lengths >= 4095 share the first bin)."""
+    """Both order paths (one-launch small sort up to 16384, two-launch sort above: count + scan by the
+    last block, then place) give a permutation in non-increasing length order (lengths >= 4095 share
+    the first bin)."""
     import torch
     e = engine("100.hmm")
     _, offsets = random_batch(50 + n % 7, n, 0, 5000)
@@ -432,6 +433,33 @@ def test_order_longest_first_sizes(n):
     assert np.array_equal(np.sort(perm), np.arange(n))
     lens = np.minimum(np.diff(offsets.astype(np.int64))[perm], 4095)
     assert np.all(lens[:-1] >= lens[1:])
+
+
+def test_order_back_to_back_sorts_reuse_scratch():
+    """Sorts queued back to back on one stream with no sync between them: each must find the
+    histogram and the last-block ticket that the previous sort left zeroed (no memset between)."""
+    import torch
+    e = engine("100.hmm")
+    dev = torch.device("cuda:0")
+    st = torch.cuda.Stream(dev)
+    cases = []
+    rng = np.random.default_rng(90)
+    for n in [200_000, 16_385, 70_001, 200_000, 1_000_003, 33_333]:
+        lens = rng.integers(0, 5000, n, dtype=np.uint64)  # the sort reads offsets only
+        offsets = np.concatenate([np.zeros(1, np.uint64), np.cumsum(lens, dtype=np.uint64)])
+        o = torch.from_numpy(offsets.view(np.int64)).to(dev)
+        order = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        cases.append((offsets, o, order))
+    torch.cuda.synchronize()
+    for _, o, order in cases:
+        e.order_longest_first(o.data_ptr(), len(order), order.data_ptr(), st.cuda_stream)
+    st.synchronize()
+    for offsets, _, order in cases:
+        n = len(order)
+        perm = order.cpu().numpy().astype(np.int64)
+        assert np.array_equal(np.sort(perm), np.arange(n))
+        lens = np.minimum(np.diff(offsets.astype(np.int64))[perm], 4095)
+        assert np.all(lens[:-1] >= lens[1:])
 
 
 def test_back_to_back_launches_self_reset_counter():
