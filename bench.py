@@ -1,7 +1,9 @@
 """bench.py -- MSV scoring throughput on MI355X (BASELINE.json metric).
 
     python bench.py --gpus N --steps K --warmup W [--config cfg3]
-    (N > 1: launched by torch.distributed.run, one process per GPU)
+    (N > 1, one process per GPU: under torch.distributed.run WORLD_SIZE must equal N; started
+    without it, bench.py runs `python -m torch.distributed.run --nproc-per-node N bench.py ...` as a
+    child process before touching torch or the GPU and exits with its status)
 
 A step = one pass of the hot path over one batch resident in HBM: the longest-first dequeue
 order (device counting sort) + ONE fused MSV kernel launch scoring every sequence of the rank's
@@ -67,6 +69,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may run on")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-order", action="store_true", help="dequeue in input order (no longest-first sort)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="check the rank layout (gloo rendezvous, no GPU) and print it from rank 0")
     return ap.parse_args()
 
 
@@ -174,15 +178,25 @@ def cpu_baseline(profile_path, codes, offsets, gpu_scores, target_s, threads):
     }
 
 
-def pmc_traffic(config: str):
-    """HBM bytes per launch from the committed rocprofv3 --pmc pass (profiles/pmc_<config>.json),
-    corrected for gfx950 FETCH_SIZE under-count as MI355X_MICROARCH.md §HBM prescribes."""
+def pmc_traffic(config: str, variant: str):
+    """HBM bytes per launch from the committed rocprofv3 --pmc passes (profiles/pmc_<config>.json,
+    tools/pmc.sh -> tools/pmc_summary.py), FETCH_SIZE corrected by the factor measured for the
+    kernel's read pattern (MI355X_MICROARCH.md §HBM; profiles/r02_fetch_calib.json).  Published only
+    when that file measured exactly the kernel this run's timed steps launch (its recorded symbol ==
+    the resident instantiation of `variant`) with a calibrated factor; otherwise None, with the reason."""
+    from hmm_fasta_viterbi_amd.kernel_names import kernel_symbol
     path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    want = kernel_symbol(variant)
     if not os.path.exists(path):
-        return None
+        return None, {"file": None, "reason": "no PMC file for this config"}
     with open(path) as f:
         d = json.load(f)
-    return d.get("hbm_bytes_per_launch")
+    src = {"file": os.path.relpath(path, ROOT), "pmc_kernel": d.get("kernel"), "timed_kernel": want}
+    if not d.get("kernel") or want not in d["kernel"]:
+        return None, {**src, "reason": "PMC file measured another kernel than the timed one"}
+    if not d.get("fetch_factor_calibrated"):
+        return None, {**src, "reason": "FETCH_SIZE factor uncalibrated"}
+    return d.get("hbm_bytes_per_launch"), src
 
 
 def issue_ceiling_tcells():
@@ -203,18 +217,59 @@ def issue_ceiling_tcells():
     return None if best is None else best * 1024 / 1000.0
 
 
-def main():
-    args = parse()
+def launcher_command(argv: list[str], gpus: int, port: int) -> list[str]:
+    """The child command that runs this bench as `gpus` ranks (one process per GPU) when it was
+    started as a plain `python bench.py --gpus N` (no torch.distributed.run around it)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def check_world(gpus: int, env=os.environ) -> str:
+    """'launch' -- spawn the ranks; 'run' -- this process is a rank (or the only one).  A rank whose
+    WORLD_SIZE differs from --gpus is an error: the line would report a GPU count nobody ran."""
+    world = env.get("WORLD_SIZE")
+    if world is None:
+        return "launch" if gpus > 1 else "run"
+    if int(world) != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {gpus}")
+    return "run"
+
+
+def launch_ranks(argv: list[str], gpus: int) -> int:
+    """Run the ranks as ONE child process tree (never exec: this process has not touched the GPU, and
+    must not replace itself) and return its exit status; rank 0 prints the JSON line to our stdout."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    return subprocess.run(launcher_command(argv, gpus, port)).returncode
+
+
+def main(args=None):
+    args = args or parse()
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    assert world == args.gpus, (world, args.gpus)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # MSV_BENCH_BACKEND=gloo + MSV_BENCH_ONE_DEVICE=1 rehearse the multi-rank path on one GPU (all ranks
     # on cuda:0, collectives on host tensors); the driver's N-GPU runs use the defaults (RCCL, one GPU
     # per rank).
     backend = os.environ.get("MSV_BENCH_BACKEND", "nccl")
+    if args.dry_run:  # the launcher's plumbing, testable on a CPU-only host
+        if world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")
+        layout = {"dry_run": True, "n_gpus": world, "ranks": dist.get_world_size() if world > 1 else 1,
+                  "local_rank": local, "config": args.config}
+        if rank == 0:
+            print(json.dumps(layout), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return layout
     if os.environ.get("MSV_BENCH_ONE_DEVICE") == "1":
         local = 0
     torch.cuda.set_device(local)
@@ -226,9 +281,13 @@ def main():
         else:
             dist.init_process_group(backend)
     cdev = dev if backend == "nccl" else torch.device("cpu")  # where collective tensors live
+    dist_world = dist.get_world_size() if world > 1 else 1
+    if dist_world != world:
+        raise SystemExit(f"bench.py: process group has {dist_world} ranks, WORLD_SIZE {world}")
 
     import hmm_fasta_viterbi_amd as msv
     from hmm_fasta_viterbi_amd import distributed
+    from hmm_fasta_viterbi_amd.kernel_names import kernel_symbol
     from hmm_fasta_viterbi_amd.synthetic import random_batch
 
     prof_name, n_cfg, lmin, lmax, seed, scaling = CONFIGS[args.config]
@@ -433,7 +492,7 @@ def main():
         cells_per_launch = residues * leng
         achieved = 3.0 * cells_per_launch / (kernel_ms * 1e-3) / 1e12
         alg_bytes = residues + n * (8 + 8 + 4 + 4) + 21 * var_g * var_s * 4
-        traffic = pmc_traffic(args.config)
+        traffic, traffic_src = pmc_traffic(args.config, variant)
         ceiling = issue_ceiling_tcells()
         per = "per GPU" if scaling == "weak" else f"in one set, {world} residue-balanced shard(s)"
         result = {
@@ -460,6 +519,9 @@ def main():
                 "parallelism": f"dp{world} (sequence shards, no data-path collective"
                                + ("; RCCL all-gather of the scores in every step)" if scaling == "strong" else ")"),
                 "kernel_variant": variant,
+                "kernel_symbol": kernel_symbol(variant),
+                "rccl_world_size": dist_world if backend == "nccl" else None,
+                "collective_backend": backend if world > 1 else None,
                 "dequeue_order": "input" if args.no_order else "longest-first",
             },
             "gcups": round(gcups, 2),
@@ -471,6 +533,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(achieved / VALU_PEAK_TOPS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "note": "fp32 add/max ops: 3 per DP cell (cells = residues x LENG); peak = 256 CU x 128 "
                         "lanes/clk x 2.4 GHz non-FMA VALU; HBM is not the bound (see hbm); traffic = "
                         "calibrated FETCH_SIZE + WRITE_SIZE per launch (profiles/pmc_<config>.json)",
@@ -524,4 +587,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    _args = parse()
+    if check_world(_args.gpus) == "launch":
+        sys.exit(launch_ranks(sys.argv[1:], _args.gpus))
+    main(_args)

@@ -1,0 +1,15 @@
+// host_cpu.h -- host-only internals shared by msv_hmm.cpp and the sanitizer drivers (host_common.cpp).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace msv_host {
+
+// MSV_HMM::run_on_sequence (MSV_HMM.cpp:74-113) on codes 0..19: emission_scores is the [20][M]
+// residue-major table of MSV_HMM.cpp:38-45 (M = LENG + 1), the score is C_L + tr_move.
+float run_on_sequence(const float* emission_scores, size_t M, float tr_B_Mk, float tr_E_C, float tr_E_J,
+                      const uint8_t* codes, size_t L);
+
+}  // namespace msv_host

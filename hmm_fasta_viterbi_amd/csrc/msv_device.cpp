@@ -358,8 +358,18 @@ static T* mapped_host(T* host) {
     return static_cast<T*>(d);
 }
 
-// Errors of a batch whose scores went straight to host memory: a bad residue leaves +inf, a
-// too-long sequence NaN (msv_kernel.hip); valid scores are finite or -inf.
+// The status of a kernel's latched error bits (msv_kernel.h kErr*), most specific first.
+static msv_status err_status(uint32_t err) {
+    if (err & msvk::kErrBadOrder) return MSV_ERR_INVALID_ARGUMENT;  // an order entry outside the batch
+    if (err & msvk::kErrBadResidue) return MSV_ERR_BAD_RESIDUE;
+    if (err & msvk::kErrTooLong) return MSV_ERR_SEQUENCE_TOO_LONG;
+    return MSV_OK;
+}
+
+// Whether a batch whose scores went straight to host memory had an error: a bad residue leaves +inf,
+// a too-long sequence or a bad order entry NaN (msv_kernel.hip); valid scores are finite or -inf.  The
+// classification of a positive answer comes from the kernel's error bits (err_status), since a NaN can
+// also come out of a bad residue's +inf meeting a -inf.
 static msv_status scan_scores(const float* scores, uint64_t n) {
     bool inf = false, nan = false;
     for (uint64_t i = 0; i < n; ++i) {
@@ -550,7 +560,8 @@ static std::vector<uint64_t> plan_pieces(const uint64_t* offsets, uint64_t n, ui
         };
         uint64_t last = std::max(end_of(std::min(want, kChunkBytes - 1)), first + 1);  // >= one sequence
         last = std::min(last, first + kMaxSeqs);
-        // a remainder shorter than half the next piece joins this one, if the chunk limit allows
+        // a remainder shorter than this piece joins it (half the next piece at the default growth of 2),
+        // if the chunk limit allows
         const uint64_t rest = offsets[n] - offsets[last];
         if (last < n && rest < want && offsets[n] - base < kChunkBytes && n - first <= kMaxSeqs) last = n;
         cut.push_back(last);
@@ -562,25 +573,6 @@ static std::vector<uint64_t> plan_pieces(const uint64_t* offsets, uint64_t n, ui
 
 extern "C" {
 
-const char* msv_status_string(msv_status s) {
-    switch (s) {
-        case MSV_OK: return "MSV_OK";
-        case MSV_ERR_INVALID_ARGUMENT: return "MSV_ERR_INVALID_ARGUMENT";
-        case MSV_ERR_IO: return "MSV_ERR_IO";
-        case MSV_ERR_PARSE: return "MSV_ERR_PARSE";
-        case MSV_ERR_BAD_RESIDUE: return "MSV_ERR_BAD_RESIDUE";
-        case MSV_ERR_SEQUENCE_TOO_LONG: return "MSV_ERR_SEQUENCE_TOO_LONG";
-        case MSV_ERR_UNSUPPORTED_MODEL: return "MSV_ERR_UNSUPPORTED_MODEL";
-        case MSV_ERR_NO_DEVICE: return "MSV_ERR_NO_DEVICE";
-        case MSV_ERR_HIP: return "MSV_ERR_HIP";
-        case MSV_ERR_OUT_OF_MEMORY: return "MSV_ERR_OUT_OF_MEMORY";
-        case MSV_ERR_RCCL: return "MSV_ERR_RCCL";
-    }
-    return "MSV_ERR_UNKNOWN";
-}
-
-const char* msv_version(void) { return "msv-mi355x 0.1.0 (gfx950)"; }
-
 msv_status msv_device_count(int* count) {
     if (!count) return MSV_ERR_INVALID_ARGUMENT;
     *count = 0;
@@ -589,32 +581,6 @@ msv_status msv_device_count(int* count) {
         *count = 0;
         return MSV_ERR_NO_DEVICE;
     }
-    return MSV_OK;
-}
-
-void msv_sequence_transitions(uint64_t L, float* tr_loop, float* tr_move) {
-    // MSV_HMM.cpp:59-64: size = seq.size() - 1; log(size / float(size + 3)), log(3 / float(size + 3))
-    const uint64_t size = L;
-    *tr_loop = std::log(size / static_cast<float>(size + 3));
-    *tr_move = std::log(3 / static_cast<float>(size + 3));
-}
-
-msv_status msv_hmm_msv_scores(const msv_hmm* hmm, float* emission_scores, float* tr_B_Mk, float* tr_E_C,
-                              float* tr_E_J) {
-    if (!hmm || !emission_scores || !tr_B_Mk || !tr_E_C || !tr_E_J) return MSV_ERR_INVALID_ARGUMENT;
-    // MSV_HMM::MSV_HMM, MSV_HMM.cpp:35-57
-    static constexpr float bg[20] = {0.0787945f, 0.0151600f, 0.0535222f, 0.0668298f, 0.0397062f,
-                                     0.0695071f, 0.0229198f, 0.0590092f, 0.0594422f, 0.0963728f,
-                                     0.0237718f, 0.0414386f, 0.0482904f, 0.0395639f, 0.0540978f,
-                                     0.0683364f, 0.0540687f, 0.0673417f, 0.0114135f, 0.0304133f};
-    const size_t M = msv_hmm_model_length(hmm);
-    const float* match = msv_hmm_match_emissions(hmm);
-    for (size_t i = 0; i < M; ++i)
-        for (size_t j = 0; j < 20; ++j) emission_scores[j * M + i] = std::log(match[i * 20 + j] / bg[j]);
-    constexpr float nu = 2.0f;
-    *tr_B_Mk = std::log(2.0f / static_cast<float>(M * (M + 1)));
-    *tr_E_C = std::log((nu - 1.0f) / nu);
-    *tr_E_J = std::log(1.0f / nu);
     return MSV_OK;
 }
 
@@ -951,9 +917,7 @@ msv_status msv_profile_check(msv_profile* p, void* stream) {
     MSV_HIP(hipStreamSynchronize(st));
     if (err) MSV_HIP(hipMemsetAsync(p->d_words + kErrWord, 0, sizeof(uint32_t), st));
     MSV_HIP(hipStreamSynchronize(st));
-    if (err & msvk::kErrBadResidue) return MSV_ERR_BAD_RESIDUE;
-    if (err & msvk::kErrTooLong) return MSV_ERR_SEQUENCE_TOO_LONG;
-    return MSV_OK;
+    return err_status(err);
 }
 
 msv_status msv_order_longest_first(msv_profile* p, const uint64_t* d_offsets, uint64_t n, uint32_t* d_order,
@@ -1207,18 +1171,18 @@ msv_status msv_profile_wait(msv_profile* p, uint64_t ticket) {
         MSV_HIP(hipEventSynchronize(a.done));
         a.pending = false;
         if (a.direct) {
-            const msv_status e = scan_scores(a.direct, a.n);
-            if (e != MSV_OK) {  // rare: clear the bits the kernel latched in the slot's error word
-                const int slot = static_cast<int>(&a - p->async);
-                MSV_HIP(hipMemsetAsync(p->d_words + kErrWord + 1 + slot, 0, sizeof(uint32_t), p->stream));
-                MSV_HIP(hipStreamSynchronize(p->stream));
-            }
-            return e;
+            if (scan_scores(a.direct, a.n) == MSV_OK) return MSV_OK;
+            // rare: classify from the bits the kernel latched in the slot's error word, and clear them
+            const int slot = static_cast<int>(&a - p->async);
+            uint32_t err = 0;
+            MSV_HIP(hipMemcpyAsync(&err, p->d_words + kErrWord + 1 + slot, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   p->stream));
+            MSV_HIP(hipMemsetAsync(p->d_words + kErrWord + 1 + slot, 0, sizeof(uint32_t), p->stream));
+            MSV_HIP(hipStreamSynchronize(p->stream));
+            const msv_status e = err_status(err);
+            return e != MSV_OK ? e : scan_scores(a.direct, a.n);
         }
-        const uint32_t err = *a.h_err;
-        if (err & msvk::kErrBadResidue) return MSV_ERR_BAD_RESIDUE;
-        if (err & msvk::kErrTooLong) return MSV_ERR_SEQUENCE_TOO_LONG;
-        return MSV_OK;
+        return err_status(*a.h_err);
     }
     return MSV_ERR_INVALID_ARGUMENT;  // unknown ticket, or already waited for
 }
@@ -1302,10 +1266,17 @@ msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profil
     if (n_profiles > 1 && n * n_profiles <= kFusedMaxSeqs) {
         uint32_t states = 0;
         bool forced = false;
+        uint32_t most = 0;  // the most times one handle is listed (each entry takes one of its counter slots)
         for (uint32_t i = 0; i < n_profiles; ++i) {
             states = std::max(states, profiles[i]->model_length - 1);
             forced |= profiles[i]->force;  // msv_profile_set_variant: that variant for every batch
+            uint32_t same = 0;
+            for (uint32_t j = 0; j < n_profiles; ++j) same += profiles[j] == profiles[i];
+            most = std::max(most, same);
         }
+        // A fused launch holds one counter slot per entry until it ends: a handle listed more often than
+        // it has slots would share a {next, waves left} pair between two sub-grids of one launch.
+        forced |= most > static_cast<uint32_t>(kLaunchSlots);
         const msvk::Variant* fv = forced ? nullptr : pick_latency_variant(states);
         if (fv && fv->grid_fn)
             return grid_fused(profiles, n_profiles, fv, d_residues, residues_len, d_offsets, n, d_order, d_scores, cs);
@@ -1451,25 +1422,6 @@ msv_status msv_pvalues_device(int device, const float* d_scores, const uint64_t*
     DeviceGuard g(device);
     if (!g.ok) return MSV_ERR_NO_DEVICE;
     MSV_HIP(msvk::launch_pvalues(d_scores, d_offsets, n, mu, lambda, d_pvalues, static_cast<hipStream_t>(stream)));
-    return MSV_OK;
-}
-
-msv_status msv_shard_bounds(const uint64_t* offsets, uint64_t n, uint32_t n_shards, uint64_t* bounds) {
-    if (!bounds || n_shards == 0 || (n && !offsets)) return MSV_ERR_INVALID_ARGUMENT;
-    bounds[0] = 0;
-    bounds[n_shards] = n;
-    if (n == 0) {
-        for (uint32_t k = 1; k < n_shards; ++k) bounds[k] = 0;
-        return MSV_OK;
-    }
-    const uint64_t total = offsets[n] - offsets[0];
-    for (uint32_t k = 1; k < n_shards; ++k) {
-        // first sequence whose END reaches the k-th residue quantile (np.searchsorted(offsets[1:], t, 'left'))
-        const unsigned __int128 q = static_cast<unsigned __int128>(total) * k / n_shards;
-        const uint64_t target = offsets[0] + static_cast<uint64_t>(q);
-        bounds[k] = static_cast<uint64_t>(std::lower_bound(offsets + 1, offsets + 1 + n, target) - (offsets + 1));
-    }
-    for (uint32_t k = 1; k <= n_shards; ++k) bounds[k] = std::min(n, std::max(bounds[k], bounds[k - 1]));
     return MSV_OK;
 }
 

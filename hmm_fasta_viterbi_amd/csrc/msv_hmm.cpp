@@ -10,6 +10,7 @@
 #include <utility>
 #include <vector>
 
+#include "host_cpu.h"
 #include "msv.h"
 #include "msv_hmm.hpp"
 
@@ -66,41 +67,13 @@ MSV_HMM& MSV_HMM::operator=(MSV_HMM&& o) noexcept {
 }
 
 Log_score MSV_HMM::run_on_sequence(const Protein_sequence& seq) {
-    // The reference's sequential CPU recurrence (MSV_HMM.cpp:74-113) over two rolling rows instead
-    // of the (L+1) x (M+5) matrix.  Same IEEE float ops in the same order and std::max argument
-    // order: Bt = B' + tr_B_Mk, M_j = e[r][j] + max(M'_{j-1}, Bt), then J, C, N, B from the new E.
-    // Only E is reduced in a different order: max is exact, and the sign of a zero E never reaches
-    // a score (E only enters E + tr_E_J / E + tr_E_C with nonzero constants).
-    constexpr float ninf = -std::numeric_limits<float>::infinity();
+    // The reference's sequential CPU recurrence (MSV_HMM.cpp:74-113), msv_host::run_on_sequence.
     const size_t L = seq.empty() ? 0 : seq.size() - 1;  // '#' sentinel (FASTA_protein_sequences.cpp:19-20)
-    float loop, move;
-    msv_sequence_transitions(L, &loop, &move);  // init_transitions_depend_on_seq, MSV_HMM.cpp:59-64
-    const size_t M = model_length_;
-    std::vector<float> prev(M, ninf), cur(M, ninf);  // [0] = the dummy M0 column, -inf on every row
     std::vector<uint8_t> codes(L);
     if (L && msv_encode_residues(seq.data() + 1, L, codes.data()) != MSV_OK)
         throw std::out_of_range("residue outside the 20 amino acids");  // amino_acid_num.at, MSV_HMM.cpp:101
-    float J = ninf, C = ninf, N = 0.0f, B = move;  // row 0 (MSV_HMM.cpp:86,96-97)
-    for (size_t i = 0; i < L; ++i) {
-        const float* e = emission_scores_.data() + static_cast<size_t>(codes[i]) * M;
-        const float Bt = B + tr_B_Mk_;
-        const float* pv = prev.data();
-        float* cv = cur.data();
-        for (size_t j = 1; j < M; ++j) cv[j] = e[j] + std::max(pv[j - 1], Bt);
-        float Ek[8] = {ninf, ninf, ninf, ninf, ninf, ninf, ninf, ninf};
-        size_t j = 1;
-        for (; j + 8 <= M; j += 8)
-            for (int q = 0; q < 8; ++q) Ek[q] = std::max(Ek[q], cv[j + q]);
-        for (; j < M; ++j) Ek[0] = std::max(Ek[0], cv[j]);
-        float E = ninf;
-        for (float x : Ek) E = std::max(E, x);
-        J = std::max(J + loop, E + tr_E_J_);
-        C = std::max(C + loop, E + tr_E_C_);
-        N = N + loop;
-        B = std::max(N + move, J + move);
-        std::swap(prev, cur);
-    }
-    return C + move;  // dp.back()[C] + tr_move; -inf for an empty sequence
+    return msv_host::run_on_sequence(emission_scores_.data(), model_length_, tr_B_Mk_, tr_E_C_, tr_E_J_, codes.data(),
+                                     L);
 }
 
 Log_score MSV_HMM::parallel_run_on_sequence(const Protein_sequence& seq, bool /*should_specialize*/) {

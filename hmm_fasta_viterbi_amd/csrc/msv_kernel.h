@@ -14,6 +14,7 @@ constexpr int kLdsLimit = 163840;
 
 constexpr uint32_t kErrBadResidue = 1u;
 constexpr uint32_t kErrTooLong = 2u;
+constexpr uint32_t kErrBadOrder = 4u;  // a dequeue-order entry >= n (caller's order, or a poisoned sort)
 
 // Residue rows of the [row][chunk][lane] float4 table that fit the 160 KiB LDS of one CU.
 constexpr int lds_rows_for(int G, int S) {
@@ -68,7 +69,7 @@ hipError_t launch_grid_variant(const Variant& v, const GridArgs& args, hipStream
 hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t n, float mu, float lambda,
                           double* pvalues, hipStream_t stream);
 
-// scratch_hist: kOrderScratchWords(nbins) words [histogram | cursors | ticket]; histogram and ticket must
+// scratch_hist: kOrderScratchWords(nbins) words [histogram | cursors | ticket | bad]; histogram and ticket must
 // be zero on entry and are zero again when the sort completes (zero them once when fresh, or after a
 // failed launch).  1024 <= nbins <= 4096 (the scan runs 1024 threads over 4 bins each).
 constexpr uint32_t kOrderScratchWords(uint32_t nbins) { return 2 * nbins + 64; }

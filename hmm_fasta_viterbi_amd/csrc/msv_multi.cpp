@@ -242,7 +242,12 @@ msv_status msv_multi_score_batch(msv_multi* m, const uint8_t* residues, const ui
     for (auto& w : workers) w.join();
     for (uint32_t k = 0; k < R; ++k)
         if (st[k] != MSV_OK) return st[k];
-    // 2. one RCCL group: shard k's scores -> device 0's buffer at offset b[k] (exact counts)
+    // 2. one RCCL group: shard k's scores -> device 0's buffer at offset b[k] (exact counts).  The
+    //    calls switch the current device per rank; the guard gives the caller's back.  (Across two or
+    //    more devices this exchange has not run on hardware yet: the test box has one GPU, where the
+    //    group is rank 0's self send/recv.)
+    DeviceGuard caller_device(m->ranks[0].device);
+    if (!caller_device.ok) return MSV_ERR_NO_DEVICE;
     MM_NCCL(ncclGroupStart());
     for (uint32_t k = 0; k < R; ++k) {
         const uint64_t cnt = b[k + 1] - b[k];

@@ -1,0 +1,43 @@
+"""Variant name -> the kernel symbol rocprofv3 reports for it (no GPU, no native library needed).
+
+The library names its instantiations `msv_g<G>_s<S>[_a<SA>]_w<W>_p<PF>_d<D>` (csrc/msv_kernel.hip,
+MSV_VARIANT / MSV_SPLIT_VARIANT); the kernel is `msvk::msv_batch_kernel<G, S, W, PF, BIG, D, SA, RPFO>`,
+BIG = the table does not fit LDS (lds_rows_for < 21) and RPFO = 2 for the zero-copy twin that
+msv_score_batch runs on page-locked residues (0 for HBM-resident launches: bench.py's timed steps).
+tools/rocprof_window.py and tools/pmc_summary.py filter dispatches on this exact symbol, and bench.py
+publishes PMC traffic only when the committed PMC file names the kernel its timed steps run.
+"""
+from __future__ import annotations
+
+import re
+
+_LDS_LIMIT = 163840
+_TABLE_ROWS = 21
+_NAME = re.compile(r"^msv_g(\d+)_s(\d+)(?:_a(\d+))?_w(\d+)_p(\d+)_d(\d+)$")
+
+
+def lds_rows_for(g: int, s: int) -> int:
+    """msv_kernel.h lds_rows_for."""
+    rows = _LDS_LIMIT // (g * s * 4)
+    return _TABLE_ROWS if rows >= _TABLE_ROWS else rows
+
+
+def parse_variant(name: str) -> dict:
+    m = _NAME.match(name)
+    if not m:
+        raise ValueError(f"not an MSV variant name: {name!r}")
+    g, s, sa, w, p, d = m.groups()
+    g, s, w, p, d = int(g), int(s), int(w), int(p), int(d)
+    sa = int(sa) if sa else 0
+    big = sa == 0 and lds_rows_for(g, s) < _TABLE_ROWS
+    return {"G": g, "S": s, "SA": sa, "waves": w, "PF": p, "D": d, "BIG": big}
+
+
+def kernel_symbol(variant: str, zero_copy: bool = False) -> str:
+    """`msv_batch_kernel<16, 88, 16, 2, false, 1, 0, 0>` for `msv_g16_s88_w16_p2_d1` (a substring of
+    the demangled name rocprofv3 prints: `void msvk::msv_batch_kernel<...>(msvk::KernelArgs)`)."""
+    v = parse_variant(variant)
+    rpfo = 2 if zero_copy else 0
+    big = "true" if v["BIG"] else "false"
+    return (f"msv_batch_kernel<{v['G']}, {v['S']}, {v['waves']}, {v['PF']}, {big}, {v['D']}, {v['SA']}, "
+            f"{rpfo}>")

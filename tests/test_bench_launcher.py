@@ -1,0 +1,48 @@
+"""bench.py's rank launcher (CPU): `python bench.py --gpus N` started without torch.distributed.run
+runs N ranks as a child process tree; under a launcher, WORLD_SIZE must equal --gpus."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from oracle_lib import ROOT
+
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_launcher_command_plumbing():
+    cmd = bench.launcher_command(["--gpus", "8", "--steps", "5", "--config", "cfg4"], 8, 29999)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd and "--master-port=29999" in cmd
+    i = cmd.index(os.path.join(ROOT, "bench.py"))
+    assert cmd[i + 1:] == ["--gpus", "8", "--steps", "5", "--config", "cfg4"]
+
+
+def test_check_world():
+    assert bench.check_world(1, {}) == "run"
+    assert bench.check_world(4, {}) == "launch"
+    assert bench.check_world(2, {"WORLD_SIZE": "2"}) == "run"
+    with pytest.raises(SystemExit):
+        bench.check_world(8, {"WORLD_SIZE": "1"})
+    with pytest.raises(SystemExit):
+        bench.check_world(1, {"WORLD_SIZE": "2"})
+
+
+def test_gpus_2_spawns_two_ranks():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--config", "cfg4"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    assert lines[0]["n_gpus"] == 2 and lines[0]["ranks"] == 2 and lines[0]["config"] == "cfg4"
+
+
+def test_world_mismatch_fails_loudly():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert p.returncode != 0 and "WORLD_SIZE=2 but --gpus 4" in p.stderr

@@ -7,6 +7,10 @@ whole batch.
         8 residue-balanced shards through msv_score_batch_multi (the one device listed 8 times) and
         distributed.shard slices must all give the same bits; >= 256 oracle samples incl. the
         longest and shortest sequences.
+  cfg2: 100.hmm x 10,000 sequences, len U[300,500] -- EVERY score bitwise against the oracle, for the
+        config's seed (1) and for bench.py's rank-0 batch (seed 1000).
+  cfg3: 1400.hmm x 100,000 sequences, len U[300,500] -- bench.py's rank-0 batch (seed 2000), EVERY
+        score bitwise against the oracle (~56 G cells on the host's threads).
   cfg5: 2405.hmm x 100,000 sequences, len U[1500,2500], seed 4 -- determinism, permutation
         invariance, >= 500 oracle samples incl. the longest and shortest sequences.
 """
@@ -90,6 +94,26 @@ def test_cfg4_full_size_three_ways():
     assert np.array_equal(bits(one[idx]), bits(want))
     for x in engines:
         x.close()
+    e.close()
+
+
+@pytest.mark.parametrize("seed", [1, 1000])
+def test_cfg2_full_size_every_score(seed):
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("100.hmm")))
+    codes, offsets = random_batch(seed, 10_000, 300, 500)
+    got = device_scores(e, codes, offsets)
+    want = OracleProfile("100").score_batch(codes, offsets, threads=ORACLE_THREADS)
+    assert np.array_equal(bits(got), bits(want))
+    assert np.array_equal(bits(e.score_batch(codes=codes, offsets=offsets)), bits(want))  # host pipeline
+    e.close()
+
+
+def test_cfg3_full_size_every_score():
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("1400.hmm")))
+    codes, offsets = random_batch(2000, 100_000, 300, 500)  # bench.py --config cfg3, rank 0
+    got = device_scores(e, codes, offsets)
+    want = OracleProfile("1400").score_batch(codes, offsets, threads=ORACLE_THREADS)
+    assert np.array_equal(bits(got), bits(want))
     e.close()
 
 

@@ -128,6 +128,32 @@ def test_bad_residue_every_large_table_layout():
     e.close()
 
 
+def test_order_entry_outside_batch_is_reported():
+    """A caller's dequeue order with an index >= n is reported (MSV_ERR_INVALID_ARGUMENT) and never
+    dereferenced; a valid order on the same profile afterwards scores exactly."""
+    import torch
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("400.hmm")))
+    codes, offsets = random_batch(41, 3000, 1, 300)
+    want = OracleProfile("400").score_batch(codes, offsets)
+    dev = torch.device("cuda:0")
+    r = torch.from_numpy(codes).to(dev)
+    o = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    s = torch.zeros(3000, dtype=torch.float32, device=dev)
+    st = torch.cuda.Stream(dev)
+    bad = torch.arange(3000, dtype=torch.int32, device=dev)
+    bad[1234] = 3000 + 77
+    torch.cuda.synchronize()
+    e.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), 3000, s.data_ptr(), bad.data_ptr(), st.cuda_stream)
+    with pytest.raises(msv.MSVError) as ex:
+        e.check(st.cuda_stream)
+    assert ex.value.name == "MSV_ERR_INVALID_ARGUMENT"
+    good = torch.arange(3000, dtype=torch.int32, device=dev).flip(0)
+    e.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), 3000, s.data_ptr(), good.data_ptr(), st.cuda_stream)
+    e.check(st.cuda_stream)
+    assert np.array_equal(bits(s.cpu().numpy()), bits(want))
+    e.close()
+
+
 def test_long_sequence_grows_table():
     e = engine("100.hmm")
     codes, offsets = random_batch(77, 2, 140000, 150000)

@@ -23,23 +23,30 @@ from collections import defaultdict
 def main():
     out, cfg = sys.argv[1], sys.argv[2]
     vals = defaultdict(list)
+    names = set()
     for path in glob.glob(os.path.join(out, "pmc*", "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
                 if "msv_batch_kernel" not in row.get("Kernel_Name", ""):
                     continue
-                vals[(row["Counter_Name"], row["Dispatch_Id"])].append(float(row["Counter_Value"]))
+                names.add(row["Kernel_Name"])
+                # per pass: Dispatch_Id restarts in every rocprofv3 run
+                vals[(row["Counter_Name"], path, row["Dispatch_Id"])].append(float(row["Counter_Value"]))
+    # Every pass must have measured ONE kernel (tools/run_kernel.py launches the resident variant only);
+    # bench.py publishes roofline.traffic only when this name is the kernel its timed steps run.
+    if len(names) != 1:
+        sys.exit(f"pmc_summary: expected one msv_batch_kernel instantiation, found {sorted(names)}")
     per = defaultdict(list)
-    for (name, disp), v in vals.items():
+    for (name, _path, _disp), v in vals.items():
         per[name].append(sum(v))
     avg = {k: sum(v) / len(v) for k, v in per.items()}
     dur = []
     for path in glob.glob(os.path.join(out, "trace", "**", "*kernel_trace.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if "msv_batch_kernel" in row["Kernel_Name"]:
+                if row["Kernel_Name"] in names:
                     dur.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
-    res = {"config": cfg, "counters_avg_per_dispatch": avg}
+    res = {"config": cfg, "kernel": next(iter(names)), "counters_avg_per_dispatch": avg}
     if dur:
         t = sum(dur) / len(dur)
         res["kernel_s_avg"] = t
