@@ -77,6 +77,9 @@ class KernelInfo(C.Structure):
         ("mid_variant", C.c_char * 64),
         ("mid_blocks", C.c_uint32),
         ("mid_max_n", C.c_uint64),
+        ("coop_variant", C.c_char * 64),
+        ("coop_blocks", C.c_uint32),
+        ("coop_max_n", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -84,6 +87,7 @@ class KernelInfo(C.Structure):
         d["variant"] = self.variant.decode()
         d["latency_variant"] = self.latency_variant.decode()
         d["mid_variant"] = self.mid_variant.decode()
+        d["coop_variant"] = self.coop_variant.decode()
         return d
 
 

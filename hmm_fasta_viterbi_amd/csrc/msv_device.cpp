@@ -240,6 +240,7 @@ struct LaunchRing {
 // One kernel instantiation with its emission table (in that variant's layout) and grid.
 struct Plan {
     const msvk::Variant* v = nullptr;
+    const msvk::CoopVariant* cv = nullptr;  // the cooperative plan (msv_coop.hip) instead of a variant
     float4* d_etab = nullptr;
     int blocks = 0;  // persistent grid size
     int groups_per_block = 0;
@@ -252,6 +253,8 @@ struct msv_profile {
     Plan lat;                     // latency plan for small batches (G = 64), may equal main's variant
     Plan mid;                     // mid-size batches (G = 32), large G = 16 profiles only
     Plan fused;                   // the table in another profile's latency layout (fused grid launches)
+    Plan coop;                    // one sequence per workgroup, the row over its waves (msv_coop.hip)
+    uint64_t coop_max_n = 0;      // batches up to this many sequences take the cooperative plan
     bool force = false;           // msv_profile_set_variant: main plan for every batch size
     uint64_t lat_max_n = 0;       // batches up to this many sequences take the latency plan
     uint64_t mid_max_n = 0;       // batches above lat_max_n and up to this many take the mid plan
@@ -459,6 +462,58 @@ static void drop_plan(Plan& plan) {
     plan = Plan{};
 }
 
+// The cooperative plan (msv_coop.hip) for batches of at most one workgroup per CU: one sequence per
+// workgroup, its row spread over 4 waves (one per SIMD) with halo states and a speculated B.  Installed
+// when a compiled CoopVariant covers the model (the whole table staged in LDS: up to 1464 states) and
+// tr_E_C == tr_E_J (the reference's nu = 2, MSV_HMM.cpp:49-53), and never under a forced variant.
+static msv_status install_coop(msv_profile* p) {
+    drop_plan(p->coop);
+    p->coop_max_n = 0;
+    if (p->force || std::memcmp(&p->tr_E_C, &p->tr_E_J, sizeof(float)) != 0) return MSV_OK;
+    const uint32_t R = p->model_length - 1;
+    int count = 0;
+    const msvk::CoopVariant* all = msvk::coop_variants(&count);
+    const msvk::CoopVariant* cv = nullptr;
+    for (int i = 0; i < count; ++i)
+        if (static_cast<uint32_t>(all[i].states()) >= R && (!cv || all[i].S < cv->S)) cv = &all[i];
+    if (!cv) return MSV_OK;
+    // [21 rows][waves][S/2 chunks][64 lanes] float2: wave w, lane l, chunk h, slot q holds global state
+    // w * (64 S - halo) - halo + l S + 2h + q + 1; states outside 1..LENG are -inf (row 20: +inf poison)
+    const int W = cv->waves, S = cv->S, H = S / 2;
+    const float ninf = -std::numeric_limits<float>::infinity();
+    const float pinf = std::numeric_limits<float>::infinity();
+    std::vector<float> tab;
+    tab.reserve(static_cast<size_t>(msvk::kTableRows) * W * H * 64 * 2);
+    for (int r = 0; r < msvk::kTableRows; ++r)
+        for (int w = 0; w < W; ++w)
+            for (int h = 0; h < H; ++h)
+                for (int l = 0; l < 64; ++l)
+                    for (int q = 0; q < 2; ++q) {
+                        const int64_t j = static_cast<int64_t>(w) * (64 * S - cv->halo) - cv->halo + l * S + 2 * h + q + 1;
+                        float val;
+                        if (r == msvk::kPoisonRow) val = pinf;
+                        else val = (j >= 1 && j <= R) ? p->emission_scores[static_cast<size_t>(r) * p->model_length + j] : ninf;
+                        tab.push_back(val);
+                    }
+    float4* d = nullptr;
+    MSV_HIP(hipMalloc(reinterpret_cast<void**>(&d), tab.size() * sizeof(float)));
+    hipError_t e = hipMemcpy(d, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return hip_status(e);
+    }
+    int cus = 0, per_cu = 0;
+    MSV_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device));
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cv->fn, W * 64, 0);
+    if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    p->coop.d_etab = d;
+    p->coop.cv = cv;
+    p->coop.blocks = cus * per_cu;
+    p->coop.groups_per_block = 1;
+    p->coop_max_n = static_cast<uint64_t>(p->coop.blocks);
+    return MSV_OK;
+}
+
 // Mid plan (G = 32, two sequences per wave) for G = 16 profiles with S >= 40 (~600-1536 states), taken
 // by batches between the latency plan's range and about one round of the main grid.  There a 16-lane
 // launch runs one partial round of 400-row sequences at ~2-3 waves per SIMD (latency-bound: ~4 ns per
@@ -498,6 +553,8 @@ static msv_status install_mid(msv_profile* p) {
 // batches that leave the SIMDs part-empty).
 static msv_status install_variant(msv_profile* p, const msvk::Variant* main_v) {
     msv_status s = install_plan(p, main_v, p->main);
+    if (s != MSV_OK) return s;
+    s = install_coop(p);
     if (s != MSV_OK) return s;
     const uint32_t states = p->model_length - 1;
     // the 16+-lane plan the latency plan is weighed against, and the plan of batches below one round of
@@ -594,6 +651,7 @@ void msv_profile_destroy(msv_profile* p) {
     (void)hipFree(p->lat.d_etab);
     (void)hipFree(p->mid.d_etab);
     (void)hipFree(p->fused.d_etab);
+    (void)hipFree(p->coop.d_etab);
     (void)hipFree(p->d_lentab);
     (void)hipFree(p->d_words);
     (void)hipFree(p->d_hist);
@@ -807,6 +865,11 @@ msv_status msv_profile_describe(const msv_profile* p, msv_kernel_info* out) {
         out->latency_blocks = static_cast<uint32_t>(p->lat.blocks);
         out->latency_max_n = p->lat_max_n;
     }
+    if (p->coop.cv) {
+        std::snprintf(out->coop_variant, sizeof(out->coop_variant), "%s", p->coop.cv->name);
+        out->coop_blocks = static_cast<uint32_t>(p->coop.blocks);
+        out->coop_max_n = p->coop_max_n;
+    }
     if (p->mid.v) {
         std::snprintf(out->mid_variant, sizeof(out->mid_variant), "%s", p->mid.v->name);
         out->mid_blocks = static_cast<uint32_t>(p->mid.blocks);
@@ -816,8 +879,10 @@ msv_status msv_profile_describe(const msv_profile* p, msv_kernel_info* out) {
 }
 
 // The plan a launch of n sequences takes: latency (n <= lat_max_n), mid (n <= mid_max_n), else main.
-static const Plan& select_plan(const msv_profile* p, uint64_t n, bool latency_ok) {
+static const Plan& select_plan(const msv_profile* p, uint64_t n, bool latency_ok, bool host_residues = false) {
     if (!latency_ok) return p->main;
+    // (not for residues read in place over PCIe: its 16-row residue blocks would wait on each one)
+    if (p->coop.cv && n <= p->coop_max_n && !host_residues) return p->coop;
     if (p->lat.v && n <= p->lat_max_n) return p->lat;
     if (p->mid.v && n <= p->mid_max_n) return p->mid;
     return p->main;
@@ -825,7 +890,8 @@ static const Plan& select_plan(const msv_profile* p, uint64_t n, bool latency_ok
 
 const char* msv_profile_variant_for(const msv_profile* p, uint64_t n) {
     if (!p || !p->main.v) return "";
-    return select_plan(p, n, true).v->name;
+    const Plan& plan = select_plan(p, n, true);
+    return plan.cv ? plan.cv->name : plan.v->name;
 }
 
 // One MSV launch.  `latency_ok`: a batch of few sequences may take the latency plan (not for the
@@ -846,7 +912,7 @@ static msv_status launch_batch(msv_profile* p, const uint8_t* d_residues, uint64
     // Small batches take the latency plan: with fewer sequences than ~4 per SIMD the launch lasts
     // one sequence's rows, and a 64-lane row is far shorter than a 16-lane one.  Mid-size ones (less
     // than one round of the main grid) take the 32-lane plan where there is one (install_variant).
-    const Plan& plan = select_plan(p, n, latency_ok);
+    const Plan& plan = select_plan(p, n, latency_ok, host_residues);
     a.etab = plan.d_etab;
     a.residues = residues_len ? d_residues : p->d_dummy;
     a.offsets = d_offsets;
@@ -862,6 +928,16 @@ static msv_status launch_batch(msv_profile* p, const uint8_t* d_residues, uint64
 
     const uint64_t want = (n + plan.groups_per_block - 1) / plan.groups_per_block;
     const int blocks = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(plan.blocks), want));
+    if (plan.cv) {  // the cooperative plan: a workgroup per sequence, no dequeue counter
+        a.errors = d_errors ? d_errors : p->d_words + kErrWord;
+        hipEvent_t t0 = p->time_start, t1 = p->time_stop;
+        p->time_start = p->time_stop = nullptr;
+        void* params[] = {&a};
+        const dim3 block(static_cast<uint32_t>(plan.cv->waves * 64));
+        MSV_HIP(t0 || t1 ? hipExtLaunchKernel(plan.cv->fn, dim3(blocks), block, params, 0, st, t0, t1, 0)
+                         : hipLaunchKernel(plan.cv->fn, dim3(blocks), block, params, 0, st));
+        return MSV_OK;
+    }
     // A slot's counters (next index, waves left) are zero between launches: zeroed at creation and
     // put back by the last wave of every launch (msv_kernel.hip).  A failed launch may leave them
     // dirty, so the slot's next launch resets them explicitly.

@@ -58,6 +58,18 @@ struct Variant {
 };
 
 const Variant* variants(int* count);
+
+// The cooperative plan (msv_coop.hip): one sequence per workgroup of `waves` waves, each wave holding
+// 64 lanes x S states of the row, the first `halo` of them a redundant copy of the previous wave's last
+// states.  Wave w's lane l, state q covers global state w * (64 S - halo) - halo + l S + q + 1; the table
+// is [21 rows][waves][S / 2][64 lanes] float2, staged whole in LDS.
+struct CoopVariant {
+    int waves, S, halo;
+    const void* fn;
+    const char* name;
+    int states() const { return waves * (64 * S - halo); }
+};
+const CoopVariant* coop_variants(int* count);
 // start/stop (optional): events updated with the kernel's own start and end (hipExtLaunchKernel), so a
 // timed launch costs no extra marker packets on the stream.
 // host_residues: args.residues is the device alias of page-locked host memory (the zero-copy twin

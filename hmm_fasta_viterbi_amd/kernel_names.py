@@ -14,6 +14,7 @@ import re
 _LDS_LIMIT = 163840
 _TABLE_ROWS = 21
 _NAME = re.compile(r"^msv_g(\d+)_s(\d+)(?:_a(\d+))?_w(\d+)_p(\d+)_d(\d+)$")
+_COOP = re.compile(r"^msv_coop_w(\d+)_s(\d+)$")
 
 
 def lds_rows_for(g: int, s: int) -> int:
@@ -35,7 +36,11 @@ def parse_variant(name: str) -> dict:
 
 def kernel_symbol(variant: str, zero_copy: bool = False) -> str:
     """`msv_batch_kernel<16, 88, 16, 2, false, 1, 0, 0>` for `msv_g16_s88_w16_p2_d1` (a substring of
-    the demangled name rocprofv3 prints: `void msvk::msv_batch_kernel<...>(msvk::KernelArgs)`)."""
+    the demangled name rocprofv3 prints: `void msvk::msv_batch_kernel<...>(msvk::KernelArgs)`);
+    `msv_coop_kernel<4, 6>` for the cooperative plan `msv_coop_w4_s6` (msv_coop.hip)."""
+    m = _COOP.match(variant)
+    if m:
+        return f"msv_coop_kernel<{m.group(1)}, {m.group(2)}>"
     v = parse_variant(variant)
     rpfo = 2 if zero_copy else 0
     big = "true" if v["BIG"] else "false"

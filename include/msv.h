@@ -155,6 +155,9 @@ typedef struct msv_kernel_info {
     char mid_variant[64];      /* mid-size plan (two sequences per wave), "" if none        */
     uint32_t mid_blocks;       /* its persistent grid                                    */
     uint64_t mid_max_n;        /* batches above latency_max_n, up to this many, take it   */
+    char coop_variant[64];     /* cooperative plan (one sequence per workgroup, its row over 4 waves), "" if none */
+    uint32_t coop_blocks;      /* its grid (one workgroup per CU)                          */
+    uint64_t coop_max_n;       /* batches of up to this many sequences take it (before the latency plan) */
 } msv_kernel_info;
 msv_status msv_profile_describe(const msv_profile* profile, msv_kernel_info* out);
 /* The kernel variant a batch of n sequences runs (msv_score_batch* / grid launches pick the plan by

@@ -46,3 +46,14 @@ def test_world_mismatch_fails_loudly():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--dry-run"],
                        capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert p.returncode != 0 and "WORLD_SIZE=2 but --gpus 4" in p.stderr
+
+
+def test_kernel_symbols():
+    from hmm_fasta_viterbi_amd.kernel_names import kernel_symbol
+    assert kernel_symbol("msv_g16_s88_w16_p2_d1") == "msv_batch_kernel<16, 88, 16, 2, false, 1, 0, 0>"
+    assert kernel_symbol("msv_g16_s88_w16_p2_d1", zero_copy=True).endswith(", 2>")
+    assert kernel_symbol("msv_g32_s76_a64_w16_p2_d1") == "msv_batch_kernel<32, 76, 16, 2, false, 1, 64, 0>"
+    assert kernel_symbol("msv_g64_s48_w16_p2_d1") == "msv_batch_kernel<64, 48, 16, 2, true, 1, 0, 0>"
+    assert kernel_symbol("msv_coop_w4_s6") == "msv_coop_kernel<4, 6>"
+    with pytest.raises(ValueError):
+        kernel_symbol("not_a_variant")

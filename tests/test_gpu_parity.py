@@ -872,3 +872,49 @@ def test_distinct_tr_E_C_and_tr_E_J():
     _, _, tEC0, tEJ0 = h.msv_scores()
     assert np.array_equal(bits(_numpy_msv(es, tBMk, tEC0, tEJ0, codes, offsets)),
                           bits(OracleProfile("100").score_batch(codes, offsets)))
+
+
+@pytest.mark.parametrize("prof", ["100", "400", "1001", "1400"])
+def test_coop_plan_edges_and_homologs(prof):
+    """The cooperative plan (msv_coop.hip: one sequence per workgroup, its row over 4 waves with halo
+    states and a speculated B) takes batches of up to one workgroup per CU.  Lengths around its
+    16-row blocks (0, 1, 15, 16, 17, 31, 32, 33, ...) and up to 3500, homologs (J >= N rows: the
+    rolled-back blocks and exact rows), bitwise against the oracle; a bad residue raises."""
+    e = engine(prof)
+    info = e.describe()
+    assert info["coop_variant"].startswith("msv_coop") and info["coop_max_n"] >= 64
+    assert e.variant_for(1) == info["coop_variant"] and e.variant_for(info["coop_max_n"] + 1) != info["coop_variant"]
+    rng = np.random.default_rng(int(prof))
+    lens = [0, 1, 2, 15, 16, 17, 31, 32, 33, 47, 48, 63, 100, 255, 256, 257, 1000, 3500]
+    parts = [rng.integers(0, 20, L, dtype=np.uint8) for L in lens]
+    ec = np.concatenate(parts)
+    eo = np.zeros(len(lens) + 1, np.uint64)
+    eo[1:] = np.cumsum(lens)
+    hc, ho = homolog_batch(msv.Profile_HMM(profile_path(prof)).match_emissions, 7, 40, 16, 900)
+    codes, offsets = concat_batches((ec, eo), (hc, ho))
+    want = OracleProfile(prof).score_batch(codes, offsets)
+    got = e.score_batch(codes=codes, offsets=offsets)
+    assert len(lens) + 40 <= info["coop_max_n"]
+    assert np.array_equal(bits(got), bits(want))
+    for k in range(len(lens) + 40):  # one sequence per call: the reference's benchmark shape
+        if k % 7 == 0:
+            one = e.score_batch(codes=codes[int(offsets[k]):int(offsets[k + 1])],
+                                offsets=np.array([0, offsets[k + 1] - offsets[k]], np.uint64))
+            assert bits(one)[0] == bits(want)[k], k
+    bad = codes.copy()
+    bad[int(offsets[len(lens) - 1]) + 1234] = 20
+    with pytest.raises(IndexError):
+        e.score_batch(codes=bad, offsets=offsets)
+    assert np.array_equal(bits(e.score_batch(codes=codes, offsets=offsets)), bits(want))
+
+
+def test_coop_plan_reference_benchmark_shape():
+    """benchmark_MSV_1400 (benchmark_MSV_1400.cpp:8-13): 1400.hmm x random_FASTA.fsa, one
+    parallel_run_on_sequence per sequence, each bitwise equal to the golden score."""
+    e = engine("1400.hmm")
+    gold = {(p, i): sc for p, i, _, sc in read_golden_tsv("random_fasta_scores.tsv")}
+    seqs = msv.FASTA_protein_sequences(os.path.join(ROOT, "data", "FASTA_files", "random_FASTA.fsa")).sequences
+    assert e.variant_for(1).startswith("msv_coop") and len(seqs) == 3
+    for k, s in enumerate(seqs):
+        got = e.parallel_run_on_sequence(s)
+        assert bits([got])[0] == bits([gold[("1400.hmm", k)]])[0]
