@@ -220,7 +220,10 @@ def test_describe_reports_every_plan():
     # mid-size batches of a large G = 16 profile: the 32-lane plan, above the latency plan's range
     assert d["mid_variant"].startswith("msv_g32_") and d["mid_blocks"] > 0
     assert d["latency_max_n"] < d["mid_max_n"] < d["blocks"] * 64
-    assert e.variant_for(1) == d["latency_variant"] and e.variant_for(d["latency_max_n"]) == d["latency_variant"]
+    # batches of at most one workgroup per CU: the cooperative plan (msv_coop.hip), then the latency plan
+    assert d["coop_variant"] == "msv_coop_w4_s6" and d["coop_max_n"] == d["coop_blocks"] >= 256
+    assert e.variant_for(1) == d["coop_variant"] == e.variant_for(d["coop_max_n"])
+    assert e.variant_for(d["coop_max_n"] + 1) == d["latency_variant"] == e.variant_for(d["latency_max_n"])
     assert e.variant_for(d["latency_max_n"] + 1) == d["mid_variant"] == e.variant_for(d["mid_max_n"])
     assert e.variant_for(d["mid_max_n"] + 1) == d["variant"] == e.variant_for(10**7)
     # 100.hmm: 4-lane groups for full batches, the 16-lane plan below 3.5 of its waves per SIMD
@@ -238,6 +241,7 @@ def test_describe_reports_every_plan():
     two_e.close()
     g32 = msv.MSV_HMM(msv.Profile_HMM(profile_path("1901.hmm"))).describe()  # main plan already 32 lanes
     assert g32["lanes_per_group"] == 32 and g32["mid_variant"] == ""
+    assert g32["coop_variant"] == ""  # 1900 states: the cooperative table would not fit LDS
     e.close()
 
 
