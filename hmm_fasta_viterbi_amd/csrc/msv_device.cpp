@@ -254,6 +254,7 @@ struct msv_profile {
     Plan mid;                     // mid-size batches (G = 32), large G = 16 profiles only
     Plan fused;                   // the table in another profile's latency layout (fused grid launches)
     Plan coop;                    // one sequence per workgroup, the row over its waves (msv_coop.hip)
+    Plan coop_fused;              // the table in another profile's cooperative layout (fused grid launches)
     uint64_t coop_max_n = 0;      // batches up to this many sequences take the cooperative plan
     bool force = false;           // msv_profile_set_variant: main plan for every batch size
     uint64_t lat_max_n = 0;       // batches up to this many sequences take the latency plan
@@ -464,37 +465,45 @@ static void drop_plan(Plan& plan) {
 
 // The cooperative plan (msv_coop.hip) for batches of at most one workgroup per CU: one sequence per
 // workgroup, its row spread over 4 waves (one per SIMD) with halo states and a speculated B.  Installed
-// when a compiled CoopVariant covers the model (the whole table staged in LDS: up to 1464 states) and
+// when a compiled CoopVariant covers the model (the whole table staged in LDS up to 1464 states, the
+// split table -- each lane's last 2-4 states read from L2 -- up to 2480) and
 // tr_E_C == tr_E_J (the reference's nu = 2, MSV_HMM.cpp:49-53), and never under a forced variant.
-static msv_status install_coop(msv_profile* p) {
-    drop_plan(p->coop);
-    p->coop_max_n = 0;
-    if (p->force || std::memcmp(&p->tr_E_C, &p->tr_E_J, sizeof(float)) != 0) return MSV_OK;
-    const uint32_t R = p->model_length - 1;
+// The smallest cooperative variant covering `states`, or nullptr.
+static const msvk::CoopVariant* pick_coop_variant(uint32_t states) {
     int count = 0;
     const msvk::CoopVariant* all = msvk::coop_variants(&count);
     const msvk::CoopVariant* cv = nullptr;
     for (int i = 0; i < count; ++i)
-        if (static_cast<uint32_t>(all[i].states()) >= R && (!cv || all[i].S < cv->S)) cv = &all[i];
-    if (!cv) return MSV_OK;
-    // [21 rows][waves][S/2 chunks][64 lanes] float2: wave w, lane l, chunk h, slot q holds global state
-    // w * (64 S - halo) - halo + l S + 2h + q + 1; states outside 1..LENG are -inf (row 20: +inf poison)
-    const int W = cv->waves, S = cv->S, H = S / 2;
+        if (static_cast<uint32_t>(all[i].states()) >= states && (!cv || all[i].S < cv->S)) cv = &all[i];
+    return cv;
+}
+
+// Lays p's table out for cooperative variant cv into `plan` (d_etab, cv).
+static msv_status install_coop_table(msv_profile* p, const msvk::CoopVariant* cv, Plan& plan) {
+    const uint32_t R = p->model_length - 1;
+    // [21 rows][waves][SA/2 chunks][64 lanes] float2 (staged in LDS): wave w, lane l, chunk h, slot q holds
+    // global state w * (64 S - halo) - halo + l S + 2h + q + 1; split variants (SA < S) append
+    // [21 rows][waves][64 lanes][S - SA] floats for the lane's states SA .. S-1 (read from L2 per row).
+    // States outside 1..LENG are -inf; row 20 is the +inf poison row.
+    const int W = cv->waves, S = cv->S, SA = cv->sa, H = SA / 2, SB = S - SA;
     const float ninf = -std::numeric_limits<float>::infinity();
     const float pinf = std::numeric_limits<float>::infinity();
+    auto value = [&](int r, int w, int l, int k) {
+        const int64_t j = static_cast<int64_t>(w) * (64 * S - cv->halo) - cv->halo + l * S + k + 1;
+        if (r == msvk::kPoisonRow) return pinf;
+        return (j >= 1 && j <= R) ? p->emission_scores[static_cast<size_t>(r) * p->model_length + j] : ninf;
+    };
     std::vector<float> tab;
-    tab.reserve(static_cast<size_t>(msvk::kTableRows) * W * H * 64 * 2);
+    tab.reserve(static_cast<size_t>(msvk::kTableRows) * W * 64 * S);
     for (int r = 0; r < msvk::kTableRows; ++r)
         for (int w = 0; w < W; ++w)
             for (int h = 0; h < H; ++h)
                 for (int l = 0; l < 64; ++l)
-                    for (int q = 0; q < 2; ++q) {
-                        const int64_t j = static_cast<int64_t>(w) * (64 * S - cv->halo) - cv->halo + l * S + 2 * h + q + 1;
-                        float val;
-                        if (r == msvk::kPoisonRow) val = pinf;
-                        else val = (j >= 1 && j <= R) ? p->emission_scores[static_cast<size_t>(r) * p->model_length + j] : ninf;
-                        tab.push_back(val);
-                    }
+                    for (int q = 0; q < 2; ++q) tab.push_back(value(r, w, l, 2 * h + q));
+    for (int r = 0; r < msvk::kTableRows && SB > 0; ++r)
+        for (int w = 0; w < W; ++w)
+            for (int l = 0; l < 64; ++l)
+                for (int i = 0; i < SB; ++i) tab.push_back(value(r, w, l, SA + i));
     float4* d = nullptr;
     MSV_HIP(hipMalloc(reinterpret_cast<void**>(&d), tab.size() * sizeof(float)));
     hipError_t e = hipMemcpy(d, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice);
@@ -502,14 +511,26 @@ static msv_status install_coop(msv_profile* p) {
         (void)hipFree(d);
         return hip_status(e);
     }
+    drop_plan(plan);
+    plan.d_etab = d;
+    plan.cv = cv;
+    plan.groups_per_block = 1;
+    return MSV_OK;
+}
+
+static msv_status install_coop(msv_profile* p) {
+    drop_plan(p->coop);
+    p->coop_max_n = 0;
+    if (p->force || std::memcmp(&p->tr_E_C, &p->tr_E_J, sizeof(float)) != 0) return MSV_OK;
+    const msvk::CoopVariant* cv = pick_coop_variant(p->model_length - 1);
+    if (!cv) return MSV_OK;
+    const msv_status st = install_coop_table(p, cv, p->coop);
+    if (st != MSV_OK) return st;
     int cus = 0, per_cu = 0;
     MSV_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device));
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cv->fn, W * 64, 0);
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cv->fn, cv->waves * 64, 0);
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
-    p->coop.d_etab = d;
-    p->coop.cv = cv;
     p->coop.blocks = cus * per_cu;
-    p->coop.groups_per_block = 1;
     p->coop_max_n = static_cast<uint64_t>(p->coop.blocks);
     return MSV_OK;
 }
@@ -652,6 +673,7 @@ void msv_profile_destroy(msv_profile* p) {
     (void)hipFree(p->mid.d_etab);
     (void)hipFree(p->fused.d_etab);
     (void)hipFree(p->coop.d_etab);
+    (void)hipFree(p->coop_fused.d_etab);
     (void)hipFree(p->d_lentab);
     (void)hipFree(p->d_words);
     (void)hipFree(p->d_hist);
@@ -1283,6 +1305,60 @@ static msv_status plan_in_layout(msv_profile* p, const msvk::Variant* v, const P
     return MSV_OK;
 }
 
+// The plan of `p` whose table is in cooperative variant cv's layout (installing it as p->coop_fused).
+static msv_status coop_plan_in_layout(msv_profile* p, const msvk::CoopVariant* cv, const Plan** out) {
+    for (const Plan* q : {&p->coop, &p->coop_fused})
+        if (q->cv == cv) {
+            *out = q;
+            return MSV_OK;
+        }
+    const msv_status s = install_coop_table(p, cv, p->coop_fused);
+    if (s != MSV_OK) return s;
+    *out = &p->coop_fused;
+    return MSV_OK;
+}
+
+// A grid of few sequences on the cooperative plan: ONE msv_coop_grid_kernel launch per 32 profiles, every
+// profile's table in the cooperative layout of the grid's largest model, one workgroup per (profile,
+// sequence).  The whole grid then lasts about as long as one sequence on one profile: benchmark_MSV's
+// 24 profiles x 3 sequences of 3,500 residues run as 72 workgroups at once.  No dequeue counters.
+static msv_status grid_coop_fused(msv_profile* const* profiles, uint32_t n_profiles, const msvk::CoopVariant* cv,
+                                  const uint8_t* d_residues, uint64_t residues_len, const uint64_t* d_offsets,
+                                  uint64_t n, const uint32_t* d_order, float* d_scores, hipStream_t cs) {
+    if (residues_len >= (1ull << 32) || !d_offsets || (residues_len && !d_residues)) return MSV_ERR_INVALID_ARGUMENT;
+    for (uint32_t first = 0; first < n_profiles; first += msvk::kGridMaxProfiles) {
+        const uint32_t count = std::min(n_profiles - first, msvk::kGridMaxProfiles);
+        msvk::GridArgs ga{};
+        ga.profiles = count;
+        ga.per_profile = static_cast<uint32_t>(n);
+        for (uint32_t j = 0; j < count; ++j) {
+            msv_profile* p = profiles[first + j];
+            const Plan* plan = nullptr;
+            const msv_status s = coop_plan_in_layout(p, cv, &plan);
+            if (s != MSV_OK) return s;
+            msvk::KernelArgs& a = ga.p[j];
+            a.etab = plan->d_etab;
+            a.residues = residues_len ? d_residues : p->d_dummy;
+            a.offsets = d_offsets;
+            a.order = d_order;
+            a.lentab = p->d_lentab;
+            a.scores = d_scores + static_cast<uint64_t>(first + j) * n;
+            a.n = n;
+            a.lentab_n = p->lentab_n;
+            a.tr_B_Mk = p->tr_B_Mk;
+            a.tr_E_C = p->tr_E_C;
+            a.tr_E_J = p->tr_E_J;
+            a.counter = p->d_words;  // (unused by the cooperative kernel)
+            a.errors = p->d_words + kErrWord;
+            a.stamps = nullptr;
+        }
+        void* params[] = {&ga};
+        MSV_HIP(hipLaunchKernel(cv->grid_fn, dim3(count * ga.per_profile), dim3(static_cast<uint32_t>(cv->waves * 64)),
+                                params, 0, cs));
+    }
+    return MSV_OK;
+}
+
 static msv_status grid_fused(msv_profile* const* profiles, uint32_t n_profiles, const msvk::Variant* v,
                              const uint8_t* d_residues, uint64_t residues_len, const uint64_t* d_offsets, uint64_t n,
                              const uint32_t* d_order, float* d_scores, hipStream_t cs) {
@@ -1341,17 +1417,21 @@ msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profil
     hipStream_t cs = stream ? static_cast<hipStream_t>(stream) : profiles[0]->stream;
     if (n_profiles > 1 && n * n_profiles <= kFusedMaxSeqs) {
         uint32_t states = 0;
-        bool forced = false;
+        bool forced = false, same_ej = true;
         uint32_t most = 0;  // the most times one handle is listed (each entry takes one of its counter slots)
         for (uint32_t i = 0; i < n_profiles; ++i) {
             states = std::max(states, profiles[i]->model_length - 1);
             forced |= profiles[i]->force;  // msv_profile_set_variant: that variant for every batch
+            same_ej &= std::memcmp(&profiles[i]->tr_E_C, &profiles[i]->tr_E_J, sizeof(float)) == 0;
             uint32_t same = 0;
             for (uint32_t j = 0; j < n_profiles; ++j) same += profiles[j] == profiles[i];
             most = std::max(most, same);
         }
         // A fused launch holds one counter slot per entry until it ends: a handle listed more often than
         // it has slots would share a {next, waves left} pair between two sub-grids of one launch.
+        const msvk::CoopVariant* cv = !forced && same_ej ? pick_coop_variant(states) : nullptr;
+        if (cv && cv->grid_fn)
+            return grid_coop_fused(profiles, n_profiles, cv, d_residues, residues_len, d_offsets, n, d_order, d_scores, cs);
         forced |= most > static_cast<uint32_t>(kLaunchSlots);
         const msvk::Variant* fv = forced ? nullptr : pick_latency_variant(states);
         if (fv && fv->grid_fn)

@@ -63,10 +63,14 @@ const Variant* variants(int* count);
 // 64 lanes x S states of the row, the first `halo` of them a redundant copy of the previous wave's last
 // states.  Wave w's lane l, state q covers global state w * (64 S - halo) - halo + l S + q + 1; the table
 // is [21 rows][waves][S / 2][64 lanes] float2, staged whole in LDS.
+// sa < S (split): the lane's first sa states in that LDS table ([21][waves][sa / 2][64] float2), its last
+// S - sa from a global table [21][waves][64][S - sa] floats that follows it.
 struct CoopVariant {
     int waves, S, halo;
     const void* fn;
     const char* name;
+    int sa;
+    const void* grid_fn;  // msv_coop_grid_kernel: several profiles' batches in one launch (GridArgs)
     int states() const { return waves * (64 * S - halo); }
 };
 const CoopVariant* coop_variants(int* count);

@@ -14,7 +14,7 @@ import re
 _LDS_LIMIT = 163840
 _TABLE_ROWS = 21
 _NAME = re.compile(r"^msv_g(\d+)_s(\d+)(?:_a(\d+))?_w(\d+)_p(\d+)_d(\d+)$")
-_COOP = re.compile(r"^msv_coop_w(\d+)_s(\d+)$")
+_COOP = re.compile(r"^msv_coop_w(\d+)_s(\d+)(?:_a(\d+))?$")
 
 
 def lds_rows_for(g: int, s: int) -> int:
@@ -37,10 +37,11 @@ def parse_variant(name: str) -> dict:
 def kernel_symbol(variant: str, zero_copy: bool = False) -> str:
     """`msv_batch_kernel<16, 88, 16, 2, false, 1, 0, 0>` for `msv_g16_s88_w16_p2_d1` (a substring of
     the demangled name rocprofv3 prints: `void msvk::msv_batch_kernel<...>(msvk::KernelArgs)`);
-    `msv_coop_kernel<4, 6>` for the cooperative plan `msv_coop_w4_s6` (msv_coop.hip)."""
+    `msv_coop_kernel<4, 6, 6>` for the cooperative plan `msv_coop_w4_s6` (msv_coop.hip), and
+    `msv_coop_kernel<4, 10, 6>` for its split form `msv_coop_w4_s10_a6`."""
     m = _COOP.match(variant)
     if m:
-        return f"msv_coop_kernel<{m.group(1)}, {m.group(2)}>"
+        return f"msv_coop_kernel<{m.group(1)}, {m.group(2)}, {m.group(3) or m.group(2)}>"
     v = parse_variant(variant)
     rpfo = 2 if zero_copy else 0
     big = "true" if v["BIG"] else "false"

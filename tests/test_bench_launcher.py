@@ -54,6 +54,7 @@ def test_kernel_symbols():
     assert kernel_symbol("msv_g16_s88_w16_p2_d1", zero_copy=True).endswith(", 2>")
     assert kernel_symbol("msv_g32_s76_a64_w16_p2_d1") == "msv_batch_kernel<32, 76, 16, 2, false, 1, 64, 0>"
     assert kernel_symbol("msv_g64_s48_w16_p2_d1") == "msv_batch_kernel<64, 48, 16, 2, true, 1, 0, 0>"
-    assert kernel_symbol("msv_coop_w4_s6") == "msv_coop_kernel<4, 6>"
+    assert kernel_symbol("msv_coop_w4_s6") == "msv_coop_kernel<4, 6, 6>"
+    assert kernel_symbol("msv_coop_w4_s10_a6") == "msv_coop_kernel<4, 10, 6>"
     with pytest.raises(ValueError):
         kernel_symbol("not_a_variant")

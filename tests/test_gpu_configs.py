@@ -241,7 +241,7 @@ def test_describe_reports_every_plan():
     two_e.close()
     g32 = msv.MSV_HMM(msv.Profile_HMM(profile_path("1901.hmm"))).describe()  # main plan already 32 lanes
     assert g32["lanes_per_group"] == 32 and g32["mid_variant"] == ""
-    assert g32["coop_variant"] == ""  # 1900 states: the cooperative table would not fit LDS
+    assert g32["coop_variant"] == "msv_coop_w4_s8_a6"  # 1901 states: the split cooperative table
     e.close()
 
 

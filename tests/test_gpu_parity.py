@@ -874,15 +874,17 @@ def test_distinct_tr_E_C_and_tr_E_J():
                           bits(OracleProfile("100").score_batch(codes, offsets)))
 
 
-@pytest.mark.parametrize("prof", ["100", "400", "1001", "1400"])
+@pytest.mark.parametrize("prof", ["100", "400", "1001", "1400", "1901", "2405"])
 def test_coop_plan_edges_and_homologs(prof):
     """The cooperative plan (msv_coop.hip: one sequence per workgroup, its row over 4 waves with halo
     states and a speculated B) takes batches of up to one workgroup per CU.  Lengths around its
     16-row blocks (0, 1, 15, 16, 17, 31, 32, 33, ...) and up to 3500, homologs (J >= N rows: the
-    rolled-back blocks and exact rows), bitwise against the oracle; a bad residue raises."""
+    rolled-back blocks and exact rows), bitwise against the oracle; a bad residue raises.  1901 and
+    2405.hmm take the split form (each lane's last states read from a global table per row)."""
     e = engine(prof)
     info = e.describe()
     assert info["coop_variant"].startswith("msv_coop") and info["coop_max_n"] >= 64
+    assert ("_a" in info["coop_variant"]) == (int(prof) > 1464)
     assert e.variant_for(1) == info["coop_variant"] and e.variant_for(info["coop_max_n"] + 1) != info["coop_variant"]
     rng = np.random.default_rng(int(prof))
     lens = [0, 1, 2, 15, 16, 17, 31, 32, 33, 47, 48, 63, 100, 255, 256, 257, 1000, 3500]
