@@ -531,7 +531,14 @@ static msv_status install_coop(msv_profile* p) {
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cv->fn, cv->waves * 64, 0);
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
     p->coop.blocks = cus * per_cu;
-    p->coop_max_n = static_cast<uint64_t>(p->coop.blocks);
+    // Up to where it beats the plan the batch would otherwise take (tools/coop_sweep.py,
+    // profiles/r03_coop_sweep.jsonl; L U[300,500], kernel ms coop / other): 1400.hmm 512 seqs 0.106 /
+    // 0.191, 1024 0.144 / 0.194, 2048 0.272 / 0.198; 1001.hmm 512 0.147 / 0.153; 1901.hmm 1024 0.243 /
+    // 0.264; 2405.hmm (L ~2000) 1024 1.19 / 1.35; 400.hmm (S = 2, 768 workgroups) 512 0.037 / 0.105, 1024
+    // 0.113 / 0.107; 100.hmm (no latency plan) 256 0.056 / 0.074, 512 0.071 / 0.074, 1024 0.099 / 0.074.
+    // So two rounds of the grid for S >= 4, one for S = 2, half of one without a latency plan.
+    const double rounds = (cv->S >= 4 ? 2.0 : 1.0) * (p->lat.v ? 1.0 : 0.5);
+    p->coop_max_n = static_cast<uint64_t>(rounds * p->coop.blocks);
     return MSV_OK;
 }
 
@@ -572,10 +579,8 @@ static msv_status install_mid(msv_profile* p) {
 // Main plan for `v`; unless forced, the latency plan (its own table layout) unless it would be the same
 // kernel, and a mid plan (install_mid; or, when the main plan has 4-lane groups, the 16-lane plan for
 // batches that leave the SIMDs part-empty).
-static msv_status install_variant(msv_profile* p, const msvk::Variant* main_v) {
+static msv_status install_variant_plans(msv_profile* p, const msvk::Variant* main_v) {
     msv_status s = install_plan(p, main_v, p->main);
-    if (s != MSV_OK) return s;
-    s = install_coop(p);
     if (s != MSV_OK) return s;
     const uint32_t states = p->model_length - 1;
     // the 16+-lane plan the latency plan is weighed against, and the plan of batches below one round of
@@ -617,6 +622,14 @@ static msv_status install_variant(msv_profile* p, const msvk::Variant* main_v) {
         return MSV_OK;
     }
     return install_mid(p);
+}
+
+// The main / mid / latency plans, then the cooperative plan in front of them (it needs to know whether a
+// latency plan exists: install_coop).
+static msv_status install_variant(msv_profile* p, const msvk::Variant* main_v) {
+    const msv_status s = install_variant_plans(p, main_v);
+    if (s != MSV_OK) return s;
+    return install_coop(p);
 }
 
 // Pieces of a host batch for msv_score_batch's copy/compute pipeline: cut[k] .. cut[k+1] is piece
@@ -844,6 +857,15 @@ msv_status msv_debug_time_next_launch(msv_profile* p, void* start, void* stop) {
 
 // Diagnostics (not in msv.h): msv_score_batch reads page-locked residues in place (1, default) or
 // copies them through the piece pipeline like pageable ones (0).
+// Diagnostics (not in msv.h): batches up to n sequences take the cooperative plan (tools/coop_sweep.py;
+// 0 turns it off).  Returns MSV_ERR_UNSUPPORTED_MODEL when the profile has no cooperative plan.
+msv_status msv_debug_set_coop_max_n(msv_profile* p, uint64_t n) {
+    if (!p) return MSV_ERR_INVALID_ARGUMENT;
+    if (!p->coop.cv) return MSV_ERR_UNSUPPORTED_MODEL;
+    p->coop_max_n = n;
+    return MSV_OK;
+}
+
 msv_status msv_debug_set_zero_copy(msv_profile* p, int on) {
     if (!p) return MSV_ERR_INVALID_ARGUMENT;
     p->zero_copy = on != 0;

@@ -221,7 +221,7 @@ def test_describe_reports_every_plan():
     assert d["mid_variant"].startswith("msv_g32_") and d["mid_blocks"] > 0
     assert d["latency_max_n"] < d["mid_max_n"] < d["blocks"] * 64
     # batches of at most one workgroup per CU: the cooperative plan (msv_coop.hip), then the latency plan
-    assert d["coop_variant"] == "msv_coop_w4_s6" and d["coop_max_n"] == d["coop_blocks"] >= 256
+    assert d["coop_variant"] == "msv_coop_w4_s6" and d["coop_max_n"] == 2 * d["coop_blocks"] >= 512
     assert e.variant_for(1) == d["coop_variant"] == e.variant_for(d["coop_max_n"])
     assert e.variant_for(d["coop_max_n"] + 1) == d["latency_variant"] == e.variant_for(d["latency_max_n"])
     assert e.variant_for(d["latency_max_n"] + 1) == d["mid_variant"] == e.variant_for(d["mid_max_n"])

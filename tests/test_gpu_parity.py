@@ -910,6 +910,17 @@ def test_coop_plan_edges_and_homologs(prof):
     assert np.array_equal(bits(e.score_batch(codes=codes, offsets=offsets)), bits(want))
 
 
+def test_coop_plan_several_sequences_per_workgroup():
+    """At its largest batch (two rounds of the grid on 1400.hmm) each workgroup scores sequences in turn."""
+    e = engine("1400.hmm")
+    info = e.describe()
+    n = info["coop_max_n"]
+    assert n > info["coop_blocks"] and e.variant_for(n) == info["coop_variant"]
+    codes, offsets = random_batch(91, n, 0, 300)
+    want = OracleProfile("1400").score_batch(codes, offsets, threads=min(16, len(os.sched_getaffinity(0))))
+    assert np.array_equal(bits(e.score_batch(codes=codes, offsets=offsets)), bits(want))
+
+
 def test_coop_plan_reference_benchmark_shape():
     """benchmark_MSV_1400 (benchmark_MSV_1400.cpp:8-13): 1400.hmm x random_FASTA.fsa, one
     parallel_run_on_sequence per sequence, each bitwise equal to the golden score."""
