@@ -932,6 +932,13 @@ static const Plan& select_plan(const msv_profile* p, uint64_t n, bool latency_ok
     return p->main;
 }
 
+// A batch that takes the cooperative plan with at most one sequence per workgroup needs no dequeue order
+// (every workgroup scores one sequence whatever the order): the host paths then skip the sort launch.
+static bool order_needless(const msv_profile* p, uint64_t n, bool host_residues) {
+    const Plan& plan = select_plan(p, n, true, host_residues);
+    return plan.cv && n <= static_cast<uint64_t>(plan.blocks);
+}
+
 const char* msv_profile_variant_for(const msv_profile* p, uint64_t n) {
     if (!p || !p->main.v) return "";
     const Plan& plan = select_plan(p, n, true);
@@ -1178,7 +1185,8 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         for (uint64_t i = 0; i <= cn; ++i) ho[i] = offsets[cut[k] + i] - base;
     }
     MSV_HIP(hipMemcpyAsync(p->d_off, p->h_off, (n + P) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    for (size_t k = 0; k < P; ++k) {
+    const bool sort = pipe || !order_needless(p, n, zres != nullptr);
+    for (size_t k = 0; k < P && sort; ++k) {
         s = msv_order_longest_first(p, p->d_off + cut[k] + k, cut[k + 1] - cut[k], p->d_order + cut[k], st);
         if (s != MSV_OK) return s;
     }
@@ -1194,7 +1202,8 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         if (pipe) MSV_HIP(hipStreamWaitEvent(c, p->events[2 + k], 0));
         const uint8_t* src = zres ? zres + base0 + lo : p->d_res + lo;
         s = launch_batch(p, bytes ? src : p->d_dummy, std::max<uint64_t>(bytes, 1), p->d_off + cut[k] + k,
-                         cut[k + 1] - cut[k], p->d_order + cut[k], dsc + cut[k], c, !pipe, nullptr, zres && bytes);
+                         cut[k + 1] - cut[k], sort ? p->d_order + cut[k] : nullptr, dsc + cut[k], c, !pipe, nullptr,
+                         zres && bytes);
         if (s != MSV_OK) return s;
     }
     if (pipe) {  // join the second compute stream (done before the last piece) back into the caller's
@@ -1256,7 +1265,8 @@ msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const 
     MSV_HIP(hipMemcpyAsync(a.d_off, a.h_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, cp));
     if (total) MSV_HIP(hipMemcpyAsync(a.d_res, residues + base, total, hipMemcpyHostToDevice, cp));
     // the order right behind the copy (it runs in the previous call's drain tail, not after it)
-    if (n) {
+    const bool sort = n && !order_needless(p, n, false);
+    if (sort) {
         s = msv_order_longest_first(p, a.d_off, n, a.d_ord, cp);
         if (s != MSV_OK) return s;
     }
@@ -1264,8 +1274,8 @@ msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const 
     // compute stream: kernel, scores and the slot's error word back to the host
     MSV_HIP(hipStreamWaitEvent(cs, a.copied, 0));
     if (n) {
-        s = launch_batch(p, total ? a.d_res : p->d_dummy, std::max<uint64_t>(total, 1), a.d_off, n, a.d_ord,
-                         direct ? direct : a.d_sc, cs, true, d_err);
+        s = launch_batch(p, total ? a.d_res : p->d_dummy, std::max<uint64_t>(total, 1), a.d_off, n,
+                         sort ? a.d_ord : nullptr, direct ? direct : a.d_sc, cs, true, d_err);
         if (s != MSV_OK) return s;
         if (!direct) MSV_HIP(hipMemcpyAsync(scores, a.d_sc, n * sizeof(float), hipMemcpyDeviceToHost, cs));
     }
@@ -1338,6 +1348,21 @@ static msv_status coop_plan_in_layout(msv_profile* p, const msvk::CoopVariant* c
     if (s != MSV_OK) return s;
     *out = &p->coop_fused;
     return MSV_OK;
+}
+
+// The cooperative variant a grid of n sequences x these profiles runs fused (grid_coop_fused), or nullptr:
+// a grid of few sequences (n x profiles <= kFusedMaxSeqs), every profile with tr_E_C == tr_E_J and no
+// forced variant, a variant covering the largest model.
+static const msvk::CoopVariant* fused_coop_variant(msv_profile* const* profiles, uint32_t n_profiles, uint64_t n) {
+    if (n_profiles < 2 || n * n_profiles > kFusedMaxSeqs) return nullptr;
+    uint32_t states = 0;
+    for (uint32_t i = 0; i < n_profiles; ++i) {
+        const msv_profile* p = profiles[i];
+        if (p->force || std::memcmp(&p->tr_E_C, &p->tr_E_J, sizeof(float)) != 0) return nullptr;
+        states = std::max(states, p->model_length - 1);
+    }
+    const msvk::CoopVariant* cv = pick_coop_variant(states);
+    return cv && cv->grid_fn ? cv : nullptr;
 }
 
 // A grid of few sequences on the cooperative plan: ONE msv_coop_grid_kernel launch per 32 profiles, every
@@ -1439,21 +1464,20 @@ msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profil
     hipStream_t cs = stream ? static_cast<hipStream_t>(stream) : profiles[0]->stream;
     if (n_profiles > 1 && n * n_profiles <= kFusedMaxSeqs) {
         uint32_t states = 0;
-        bool forced = false, same_ej = true;
+        bool forced = false;
         uint32_t most = 0;  // the most times one handle is listed (each entry takes one of its counter slots)
         for (uint32_t i = 0; i < n_profiles; ++i) {
             states = std::max(states, profiles[i]->model_length - 1);
             forced |= profiles[i]->force;  // msv_profile_set_variant: that variant for every batch
-            same_ej &= std::memcmp(&profiles[i]->tr_E_C, &profiles[i]->tr_E_J, sizeof(float)) == 0;
             uint32_t same = 0;
             for (uint32_t j = 0; j < n_profiles; ++j) same += profiles[j] == profiles[i];
             most = std::max(most, same);
         }
+        const msvk::CoopVariant* cv = fused_coop_variant(profiles, n_profiles, n);
+        if (cv)
+            return grid_coop_fused(profiles, n_profiles, cv, d_residues, residues_len, d_offsets, n, d_order, d_scores, cs);
         // A fused launch holds one counter slot per entry until it ends: a handle listed more often than
         // it has slots would share a {next, waves left} pair between two sub-grids of one launch.
-        const msvk::CoopVariant* cv = !forced && same_ej ? pick_coop_variant(states) : nullptr;
-        if (cv && cv->grid_fn)
-            return grid_coop_fused(profiles, n_profiles, cv, d_residues, residues_len, d_offsets, n, d_order, d_scores, cs);
         forced |= most > static_cast<uint32_t>(kLaunchSlots);
         const msvk::Variant* fv = forced ? nullptr : pick_latency_variant(states);
         if (fv && fv->grid_fn)
@@ -1550,11 +1574,13 @@ msv_status msv_score_grid(msv_profile* const* profiles, uint32_t n_profiles, con
     const uint8_t* d_res = zres ? zres : p0->d_res;
     if (bytes && !zres) MSV_HIP(hipMemcpyAsync(p0->d_res, residues + offsets[0], bytes, hipMemcpyHostToDevice, st));
     MSV_HIP(hipMemcpyAsync(p0->d_off, p0->h_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    msv_status s = msv_order_longest_first(p0, p0->d_off, n, p0->d_order, st);
+    // (a fused cooperative grid runs one workgroup per sequence: no dequeue order to sort)
+    const bool sort = !zres ? fused_coop_variant(profiles, n_profiles, n) == nullptr : true;
+    msv_status s = sort ? msv_order_longest_first(p0, p0->d_off, n, p0->d_order, st) : MSV_OK;
     if (s != MSV_OK) return s;
     float* const dsc = direct ? direct : p0->d_scores;
     s = msv_score_grid_device(profiles, n_profiles, bytes ? d_res : p0->d_dummy, std::max<uint64_t>(bytes, 1),
-                              p0->d_off, n, p0->d_order, dsc, st);
+                              p0->d_off, n, sort ? p0->d_order : nullptr, dsc, st);
     if (s != MSV_OK) return s;
     if (!direct) MSV_HIP(hipMemcpyAsync(scores, p0->d_scores, total * sizeof(float), hipMemcpyDeviceToHost, st));
     drain.armed = false;
