@@ -931,3 +931,40 @@ def test_coop_plan_reference_benchmark_shape():
     for k, s in enumerate(seqs):
         got = e.parallel_run_on_sequence(s)
         assert bits([got])[0] == bits([gold[("1400.hmm", k)]])[0]
+
+
+def test_coop_plan_device_order_async_and_shards():
+    """The cooperative plan under the other entry points: a caller's dequeue order on device buffers (a
+    valid permutation scores exactly, an entry >= n is reported as MSV_ERR_INVALID_ARGUMENT), the
+    asynchronous host path (no sort for one sequence per workgroup), and residue-balanced shards of a
+    small batch through msv_score_batch_multi -- all bitwise against the oracle."""
+    import torch
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("1001.hmm")))
+    n = 120
+    assert e.variant_for(n).startswith("msv_coop")
+    codes, offsets = random_batch(93, n, 0, 700)
+    want = OracleProfile("1001").score_batch(codes, offsets)
+    dev = torch.device("cuda:0")
+    r = torch.from_numpy(codes).to(dev)
+    o = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    s = torch.zeros(n, dtype=torch.float32, device=dev)
+    st = torch.cuda.Stream(dev)
+    perm = torch.from_numpy(np.random.default_rng(5).permutation(n).astype(np.int32)).to(dev)
+    torch.cuda.synchronize()
+    e.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), n, s.data_ptr(), perm.data_ptr(), st.cuda_stream)
+    e.check(st.cuda_stream)
+    assert np.array_equal(bits(s.cpu().numpy()), bits(want))
+    bad = perm.clone()
+    bad[17] = n + 3
+    e.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), n, s.data_ptr(), bad.data_ptr(), st.cuda_stream)
+    with pytest.raises(msv.MSVError) as ex:
+        e.check(st.cuda_stream)
+    assert ex.value.name == "MSV_ERR_INVALID_ARGUMENT"
+    out = np.zeros(n, np.float32)
+    t = e.score_batch_async(codes, offsets, out)
+    assert np.array_equal(bits(e.wait(t)), bits(want))
+    engines = [msv.MSV_HMM(msv.Profile_HMM(profile_path("1001.hmm")), device=0) for _ in range(3)]
+    assert np.array_equal(bits(msv.score_batch_multi(engines, codes=codes, offsets=offsets)), bits(want))
+    for x in engines:
+        x.close()
+    e.close()
