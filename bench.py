@@ -383,25 +383,25 @@ def main(args=None):
     host_pinned_copy, copy_scores = host_rate(pinned_codes, torch.empty(n, dtype=torch.float32).pin_memory().numpy())
     _native.lib().msv_debug_set_zero_copy(engine._p, 1)
 
-    # Stream of batches (serving): msv_score_batch_async keeps two calls in flight, so each call's H2D
-    # runs under the previous call's kernel; scores land in pinned host arrays.
-    outs = [torch.empty(n, dtype=torch.float32).pin_memory().numpy() for _ in range(2)]
+    # Stream of batches (serving): msv_score_batch_async keeps three calls in flight, so the H2D of the
+    # next calls runs back to back under the current call's kernel; scores land in pinned host arrays.
+    outs = [torch.empty(n, dtype=torch.float32).pin_memory().numpy() for _ in range(3)]
 
     def streamed_rate():
         for _ in range(3):
             engine.wait(engine.score_batch_async(pinned_codes, offsets, outs[0]))
         t = time.perf_counter()
-        prev = None
+        inflight = []
         for k in range(args.steps):
-            cur = engine.score_batch_async(pinned_codes, offsets, outs[k % 2])
-            if prev is not None:
-                engine.wait(prev)
-            prev = cur
-        engine.wait(prev)
+            inflight.append(engine.score_batch_async(pinned_codes, offsets, outs[k % 3]))
+            if len(inflight) == 3:
+                engine.wait(inflight.pop(0))
+        for tk in inflight:
+            engine.wait(tk)
         return residues * args.steps / (time.perf_counter() - t) / 1e6
 
     host_streamed = streamed_rate()
-    streamed_scores = outs[(args.steps - 1) % 2].copy()
+    streamed_scores = outs[(args.steps - 1) % 3].copy()
 
     # Information, never `value` (run BEFORE the timed steps, so those stay the last K MSV dispatches for
     # tools/rocprof_window.py): K steps as a stream of resident batches alternating over two streams, so
@@ -568,8 +568,8 @@ def main(args=None):
                         "place over PCIe (zero-copy), scores written to the pinned destination by the "
                         "kernel; rank 0, warm, mean of `steps` calls); host_pinned_copy_pipeline = the same "
                         "call with the residues copied in pieces under the kernels; host_pinned_streamed = the same batch as a stream of `steps` "
-                        "msv_score_batch_async calls, two in flight (copy of one under the kernel of the "
-                        "other, kernels on alternating streams); resident_two_streams = `steps` resident "
+                        "msv_score_batch_async calls, three in flight (the copies of the next calls under the "
+                        "current kernel, kernels on alternating streams); resident_two_streams = `steps` resident "
                         "steps before the timed ones, alternating over two streams so each step's blocks fill the previous "
                         "step's drain tail; `value` is the HBM-resident rate of serial steps the bench "
                         "contract prescribes",

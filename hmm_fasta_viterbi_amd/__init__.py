@@ -221,7 +221,7 @@ class MSV_HMM:
 
     def score_batch_async(self, codes: np.ndarray, offsets: np.ndarray, out: np.ndarray | None = None) -> int:
         """Enqueue a host batch (msv_score_batch_async) and return a ticket; `wait(ticket)` returns
-        the scores.  At most two calls outstanding; pinned arrays (torch pin_memory().numpy()) make
+        the scores.  At most three calls outstanding; pinned arrays (torch pin_memory().numpy()) make
         the copies overlap the previous call's kernel.  The arrays are held until the wait."""
         codes = np.ascontiguousarray(codes, np.uint8)
         offsets = np.ascontiguousarray(offsets, np.uint64)

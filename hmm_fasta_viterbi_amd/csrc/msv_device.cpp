@@ -32,7 +32,7 @@ constexpr uint32_t kOrderBins = 4096;  // lengths >= 4095 share the longest bin
 // streams differ).  d_words: [2k, 2k+1] = slot k's counters, [kErrWord] = sticky error bits,
 // [kErrWord + 1 + a] = the error bits of asynchronous staging slot a (msv_score_batch_async).
 constexpr int kLaunchSlots = 8;
-constexpr int kAsyncSlots = 2;
+constexpr int kAsyncSlots = 3;
 constexpr int kErrWord = 2 * kLaunchSlots;
 constexpr int kWords = kErrWord + 1 + kAsyncSlots + 1;
 // Every launch addresses < 2^32 residue bytes.
@@ -1259,20 +1259,23 @@ msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const 
     uint32_t* d_err = p->d_words + kErrWord + 1 + slot;
     // Consecutive calls alternate over two compute streams, so a call's kernel fills the CUs that the
     // previous call's drain tail frees instead of starting after the whole previous kernel.
-    if ((slot & 1) && !p->stream2) MSV_HIP(hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking));
-    hipStream_t cp = p->copy_stream, cs = (slot & 1) ? p->stream2 : p->stream;
-    // copy stream: this call's inputs (they overlap the previous call's kernel on the compute stream)
+    const bool odd = (p->next_ticket & 1) != 0;
+    if (odd && !p->stream2) MSV_HIP(hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking));
+    hipStream_t cp = p->copy_stream, cs = odd ? p->stream2 : p->stream;
+    // copy stream: this call's inputs (they overlap the earlier calls' kernels on the compute streams).
+    // Nothing but copies goes on it: a kernel there (the order, as in round 2) waits for the running MSV
+    // grid to drain before it can start, and every later call's copies queued behind it.
     MSV_HIP(hipMemcpyAsync(a.d_off, a.h_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, cp));
     if (total) MSV_HIP(hipMemcpyAsync(a.d_res, residues + base, total, hipMemcpyHostToDevice, cp));
-    // the order right behind the copy (it runs in the previous call's drain tail, not after it)
+    MSV_HIP(hipEventRecord(a.copied, cp));
+    // compute stream: order, kernel, scores and the slot's error word back to the host (the order runs
+    // in the previous call's drain tail: that call's kernel is on the other compute stream)
+    MSV_HIP(hipStreamWaitEvent(cs, a.copied, 0));
     const bool sort = n && !order_needless(p, n, false);
     if (sort) {
-        s = msv_order_longest_first(p, a.d_off, n, a.d_ord, cp);
+        s = msv_order_longest_first(p, a.d_off, n, a.d_ord, cs);
         if (s != MSV_OK) return s;
     }
-    MSV_HIP(hipEventRecord(a.copied, cp));
-    // compute stream: kernel, scores and the slot's error word back to the host
-    MSV_HIP(hipStreamWaitEvent(cs, a.copied, 0));
     if (n) {
         s = launch_batch(p, total ? a.d_res : p->d_dummy, std::max<uint64_t>(total, 1), a.d_off, n,
                          sort ? a.d_ord : nullptr, direct ? direct : a.d_sc, cs, true, d_err);

@@ -197,9 +197,9 @@ msv_status msv_score_batch(msv_profile* profile, const uint8_t* residues, const 
  * inputs on the profile's copy stream and the order, kernel and score D2H on one of its two compute
  * streams (consecutive calls alternate, so a call's kernel fills the previous one's drain tail), and
  * returns at once with a ticket; msv_profile_wait(ticket) blocks until that call's scores are in
- * `scores` and returns its kernel-latched errors.  Two staging sets, so the copy of call k+1 runs
- * under the kernel of call k; at most 2 calls may be outstanding (a third returns
- * MSV_ERR_INVALID_ARGUMENT until the oldest is waited for).  The caller keeps residues/offsets
+ * `scores` and returns its kernel-latched errors.  Three staging sets, so the copies of the next calls
+ * run back to back under the kernels of the earlier ones; at most 3 calls may be outstanding (a fourth
+ * returns MSV_ERR_INVALID_ARGUMENT until the oldest is waited for).  The caller keeps residues/offsets
  * unchanged and does not read scores until the wait; pinned (page-locked) host buffers make the
  * copies truly asynchronous, and pinned `scores` are written by the kernel directly (no D2H; that
  * call's errors are then read from its scores: +inf = bad residue, NaN = too long).  One launch per

@@ -246,9 +246,9 @@ def test_describe_reports_every_plan():
 
 
 def test_async_stream_of_batches():
-    """msv_score_batch_async / msv_profile_wait: two calls in flight (copy of one under the kernel
-    of the other), results equal to the synchronous path; a bad residue is reported by the wait of
-    ITS call only; a third outstanding call is refused."""
+    """msv_score_batch_async / msv_profile_wait: three calls in flight (the copies of the later ones
+    under the kernel of the first), results equal to the synchronous path; a bad residue is reported
+    by the wait of ITS call only; a fourth outstanding call is refused."""
     import torch
     from hmm_fasta_viterbi_amd._native import MSVError
     e = msv.MSV_HMM(msv.Profile_HMM(profile_path("1400.hmm")))
@@ -259,8 +259,9 @@ def test_async_stream_of_batches():
     got = []
     for k, (c, o) in enumerate(pinned):
         tickets.append(e.score_batch_async(c, o))
-        if k >= 1:
-            got.append(e.wait(tickets[k - 1]))
+        if k >= 2:
+            got.append(e.wait(tickets[k - 2]))
+    got.append(e.wait(tickets[-2]))
     got.append(e.wait(tickets[-1]))
     for k, (g, w) in enumerate(zip(got, want)):
         assert np.array_equal(bits(g), bits(w)), k
@@ -269,11 +270,13 @@ def test_async_stream_of_batches():
     bad_c[int(batches[0][1][9]) + 1] = 25
     t_bad = e.score_batch_async(bad_c, batches[0][1])
     t_ok = e.score_batch_async(batches[2][0], batches[2][1])
+    t_ok2 = e.score_batch_async(batches[5][0], batches[5][1])
     with pytest.raises(MSVError):
-        e.score_batch_async(batches[3][0], batches[3][1])  # two already outstanding
+        e.score_batch_async(batches[3][0], batches[3][1])  # three already outstanding
     with pytest.raises(IndexError):
         e.wait(t_bad)
     assert np.array_equal(bits(e.wait(t_ok)), bits(want[2]))
+    assert np.array_equal(bits(e.wait(t_ok2)), bits(want[5]))
     with pytest.raises(MSVError):
         e.wait(t_ok)  # already waited for
     e.close()

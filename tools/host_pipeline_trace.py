@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--calls", type=int, default=30)
     ap.add_argument("--mark", type=int, default=3)
     ap.add_argument("--streamed", type=int, default=0,
-                    help="after the one-call passes: a 1 ms gap, then this many msv_score_batch_async calls, two in flight")
+                    help="after the one-call passes: a 1 ms gap, then this many msv_score_batch_async calls, three in flight")
     a = ap.parse_args()
     import torch
     import bench  # noqa: F401  (sets GPU_MAX_HW_QUEUES before HIP starts)
@@ -40,15 +40,16 @@ def main():
         e.score_batch(codes=pinned, offsets=offsets, out=pout)
         print(f"call {k}: {(time.perf_counter() - t) * 1e3:.3f} ms", flush=True)
     if a.streamed:
-        outs = [torch.empty(n, dtype=torch.float32).pin_memory().numpy() for _ in range(2)]
+        outs = [torch.empty(n, dtype=torch.float32).pin_memory().numpy() for _ in range(3)]
         time.sleep(0.001)
         t = time.perf_counter()
-        prev = e.score_batch_async(pinned, offsets, outs[0])
-        for k in range(1, a.streamed):
-            cur = e.score_batch_async(pinned, offsets, outs[k % 2])
-            e.wait(prev)
-            prev = cur
-        e.wait(prev)
+        inflight = []
+        for k in range(a.streamed):
+            inflight.append(e.score_batch_async(pinned, offsets, outs[k % 3]))
+            if len(inflight) == 3:
+                e.wait(inflight.pop(0))
+        for tk in inflight:
+            e.wait(tk)
         dt = (time.perf_counter() - t) * 1e3
         print(f"streamed: {a.streamed} calls {dt:.3f} ms = {dt / a.streamed:.3f} ms per call", flush=True)
 
