@@ -279,6 +279,7 @@ struct msv_profile {
     uint32_t pipe_first_den = 4, pipe_growth = 2;  // piece sizes: total / first_den, then x growth
     uint32_t pipe_streams = 2;                      // compute streams the pieces alternate over
     bool zero_copy = true;  // page-locked residues read in place (msv_debug_set_zero_copy turns it off)
+    bool zc_wide = true;    // ... by the wide-block twins of residue-block variants (msv_debug_set_zero_copy 2: off)
     // msv_score_batch_async: kAsyncSlots staging sets, so the H2D of one call runs under the kernel
     // of the call before it
     struct AsyncSlot {
@@ -866,9 +867,12 @@ msv_status msv_debug_set_coop_max_n(msv_profile* p, uint64_t n) {
     return MSV_OK;
 }
 
+// on: 0 = page-locked residues are copied (pipeline), 1 = read in place, 2 = read in place but without the
+// wide-block twins (A/B of the 64-byte superblock requests against the 16-byte block requests).
 msv_status msv_debug_set_zero_copy(msv_profile* p, int on) {
-    if (!p) return MSV_ERR_INVALID_ARGUMENT;
+    if (!p || on < 0 || on > 2) return MSV_ERR_INVALID_ARGUMENT;
     p->zero_copy = on != 0;
+    p->zc_wide = on != 2;
     return MSV_OK;
 }
 
@@ -1000,7 +1004,11 @@ static msv_status launch_batch(msv_profile* p, const uint8_t* d_residues, uint64
     p->kernels.dirty[k] = true;
     hipEvent_t t0 = p->time_start, t1 = p->time_stop;
     p->time_start = p->time_stop = nullptr;
-    MSV_HIP(msvk::launch_variant(*plan.v, dim3(blocks), a, st, t0, t1, host_residues));
+    // the twin of a residue-block variant (rows of <= 40 states) reads 4-byte superblock words, clamped
+    // to the buffer only from 4 bytes up: it takes buffers of at least 64 bytes
+    const bool wide = plan.v->S <= 40;  // (twins of rows > 40 states prefetch two rows; see zc_fn)
+    const bool twin = host_residues && (!wide || (p->zc_wide && residues_len >= 64));
+    MSV_HIP(msvk::launch_variant(*plan.v, dim3(blocks), a, st, t0, t1, twin));
     p->kernels.dirty[k] = false;
     MSV_HIP(p->kernels.release(k, st, lazy_stream(p, st)));
     return MSV_OK;
@@ -1210,7 +1218,16 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         MSV_HIP(hipEventRecord(p->events[P + 3], cs[1]));
         MSV_HIP(hipStreamWaitEvent(st, p->events[P + 3], 0));
     }
-    if (!direct) MSV_HIP(hipMemcpyAsync(scores, p->d_scores, n * sizeof(float), hipMemcpyDeviceToHost, st));
+    if (direct) {
+        // scores in page-locked memory: every error leaves a score that is +inf or NaN (scan_scores), so
+        // the error word is read only on that rare path (its D2H was a blit launch + 4 us per call)
+        MSV_HIP(hipStreamSynchronize(st));  // also: the pinned h_off is rewritten by the next call
+        drain.armed = false;
+        if (scan_scores(direct, n) == MSV_OK) return MSV_OK;
+        const msv_status e = msv_profile_check(p, st);  // reads, clears and reports the latched error bits
+        return e != MSV_OK ? e : scan_scores(direct, n);
+    }
+    MSV_HIP(hipMemcpyAsync(scores, p->d_scores, n * sizeof(float), hipMemcpyDeviceToHost, st));
     MSV_HIP(hipMemcpyAsync(h_err, p->d_words + kErrWord, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     MSV_HIP(hipStreamSynchronize(st));  // also: the pinned h_off is rewritten by the next call
     drain.armed = false;

@@ -10,6 +10,9 @@ namespace msvk {
 constexpr int kAminoAcids = 20;
 constexpr int kPoisonRow = 20;   // codes >= 20 are clamped here; the row is +inf -> score +inf -> error
 constexpr int kTableRows = 21;   // 20 residues + poison row
+// RPFO value (msv_batch_kernel's last template parameter) that selects the wide-block zero-copy twin
+// of a residue-block variant (msv_kernel_impl.h zc_fn)
+constexpr int kWideBlocks = 64;
 constexpr int kLdsLimit = 163840;
 
 constexpr uint32_t kErrBadResidue = 1u;

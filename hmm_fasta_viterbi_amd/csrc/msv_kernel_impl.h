@@ -143,6 +143,15 @@ struct Stream {
     bool junk;        // current "sequence" is an empty/too-long record: discard its row
 };
 
+// WIDE blocks (zero-copy twins of BLK variants, one stream per lane group): the current and next 64-row
+// superblocks (one dword per lane), the next superblock's address and the load clamp, the index of the
+// next block, the next block (taken from the current superblock by ds_bpermute).  Kept out of Stream:
+// any new Stream field moved the register assignment of every other variant.
+struct WideBlocks {
+    uint32_t wcur, wnext, nsh, snext, e3, wr, nxw;  // (nsh: wnext's pending shift, see load_w)
+};
+struct NoWideBlocks {};
+
 // Per-row working set of one stream.
 template <int PF>
 struct RowCtx {
@@ -201,10 +210,17 @@ constexpr const void* grid_fn() {
 // prefetch hides an HBM/L2 load, not a PCIe round trip at each 128-B line: cfg3 read in place 2.945 vs
 // 2.856 ms with the twin, while from HBM it is 0.3-0.7% slower on 1400/1901.hmm (2% faster on
 // 1001.hmm) -- profiles/r02_zero_copy_twins.jsonl.  Split variants already prefetch two rows.
+// Rows of up to 40 states already read residue blocks (one 16-byte request per group per 16 rows):
+// the twins of those with two-rows-ahead emission rings (PF <= 2) read WIDE blocks, 64-byte requests
+// (msv_kernel_body.inc): cfg2's call 0.228 -> 0.223 ms, 200.hmm x 2000 (64-lane plan) 0.126 -> 0.121 ms;
+// the whole-row-ring variants (PF = S/4 > 2) were slower with them (400.hmm x 20k 0.415 -> 0.46 ms) and
+// keep their 16-byte blocks -- profiles/r03_ab_zero_copy_wide.jsonl.
 template <int G, int S, int WAVES, int PF, bool BIG, int D, int SA = 0>
 constexpr const void* zc_fn() {
     if constexpr ((G == 16 || G == 32) && D == 1 && !BIG && SA == 0 && S > 40)
         return reinterpret_cast<const void*>(&msv_batch_kernel<G, S, WAVES, PF, BIG, D, SA, 2>);
+    else if constexpr (G >= 16 && D == 1 && !BIG && SA == 0 && residue_prefetch<S>() > 1 && PF <= 2)
+        return reinterpret_cast<const void*>(&msv_batch_kernel<G, S, WAVES, PF, BIG, D, SA, kWideBlocks>);
     else return nullptr;
 }
 

@@ -346,6 +346,95 @@ def test_zero_copy_twin_variants(prof):
     e.close()
 
 
+def _wide_edge_batch(prof, seed):
+    """Lengths around the 16-row blocks and 64-row superblocks of the wide twins (0-5, 15-17, ..., 127-129),
+    random ones, and homologs (J >= N rows), shuffled so sequences begin at every phase of the row loop."""
+    edges = [0, 1, 2, 3, 4, 5, 15, 16, 17, 31, 32, 33, 47, 48, 49, 63, 64, 65, 79, 80, 81, 127, 128, 129, 200]
+    rng = np.random.default_rng(seed)
+    lens = np.array(edges * 3 + list(rng.integers(0, 400, 150)), np.int64)
+    codes = rng.integers(0, 20, int(lens.sum())).astype(np.uint8)
+    offsets = np.zeros(len(lens) + 1, np.uint64)
+    offsets[1:] = np.cumsum(lens)
+    hc, ho = homolog_batch(msv.Profile_HMM(profile_path(prof + ".hmm")).match_emissions, seed + 1, 40, 1, 300)
+    codes, offsets = concat_batches((codes, offsets), (hc, ho))
+    perm = rng.permutation(len(offsets) - 1)
+    return subset(codes, offsets, perm)
+
+
+def test_zero_copy_wide_blocks_every_short_row_variant():
+    """The zero-copy twins of residue-block variants (rows of <= 40 states, G >= 16) read 64-row
+    superblocks as unaligned dwords (msv_kernel_body.inc WIDE): every such variant, forced, on residues in
+    a page-locked buffer of exactly the batch's size (the last sequence ends at the allocation's end),
+    equals the oracle bitwise -- lengths around every block/superblock edge, homologs, all begin phases
+    -- and so does the 16-byte-block form (msv_debug_set_zero_copy 2)."""
+    import ctypes as C
+    from hmm_fasta_viterbi_amd import _native
+
+    def _variant_shape(name):  # msv_g<G>_s<S>_...
+        parts = name.split("_")
+        return int(parts[1][1:]), int(parts[2][1:])
+    L = _native.lib()
+    L.msv_debug_set_zero_copy.argtypes = [C.c_void_p, C.c_int]
+    names = [n for n in msv.MSV_HMM.variants() if not n.startswith("exp")]
+    short = [n for n in names if _variant_shape(n)[0] >= 16 and _variant_shape(n)[1] <= 40
+             and "_a" not in n and "_d1" in n]
+    assert len(short) >= 20
+    by_prof = {}
+    lengs = {p: msv.Profile_HMM(profile_path(p + ".hmm")).model_length - 1
+             for p in ("100", "200", "300", "400", "500", "600", "700", "800", "900", "1001", "1100", "1200")}
+    for name in short:
+        g, s = _variant_shape(name)
+        fits = [p for p in lengs if lengs[p] <= g * s]
+        if fits:  # (16 x 4 covers no real profile: the smallest has 100 states)
+            by_prof.setdefault(max(fits, key=lambda p: lengs[p]), []).append(name)
+    assert sum(len(v) for v in by_prof.values()) >= 20
+    for k, (prof, vs) in enumerate(sorted(by_prof.items())):
+        codes, offsets = _wide_edge_batch(prof, 900 + k)
+        want = OracleProfile(prof).score_batch(codes, offsets)
+        pc = msv.pinned_empty(codes.size, np.uint8)
+        pc[:] = codes
+        out = msv.pinned_empty(len(want), np.float32)
+        e = msv.MSV_HMM(msv.Profile_HMM(profile_path(prof + ".hmm")))
+        for name in vs:
+            e.set_variant(name)
+            for mode in (1, 2):
+                assert L.msv_debug_set_zero_copy(e._p, mode) == 0
+                assert np.array_equal(bits(e.score_batch(codes=pc, offsets=offsets)), bits(want)), (prof, name, mode)
+                got = e.score_batch(codes=pc, offsets=offsets, out=out)  # page-locked scores too
+                assert got is out and np.array_equal(bits(out), bits(want)), (prof, name, mode)
+        e.close()
+
+
+def test_zero_copy_wide_blocks_small_buffers_and_errors():
+    """Buffers of 63 bytes (too small for the dword twin: the ordinary variant runs) and of 64 and 65
+    bytes (the twin, its clamp at the buffer's first and last bytes), a bad residue inside a superblock
+    (raises, and the next call is clean), and cfg2's full batch from page-locked memory against the
+    resident launch."""
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("100.hmm")))
+    o = OracleProfile("100")
+    rng = np.random.default_rng(77)
+    for total in (63, 64, 65, 66, 67, 130):
+        for lens in ([total], [1, total - 1], [total - 3, 3], [20, 20, total - 40] if total > 40 else [total]):
+            codes = rng.integers(0, 20, total).astype(np.uint8)
+            offsets = np.zeros(len(lens) + 1, np.uint64)
+            offsets[1:] = np.cumsum(lens)
+            pc = msv.pinned_empty(total, np.uint8)
+            pc[:] = codes
+            assert np.array_equal(bits(e.score_batch(codes=pc, offsets=offsets)), bits(o.score_batch(codes, offsets)))
+    codes, offsets = random_batch(1, 10_000, 300, 500)  # cfg2 (BASELINE configs[1]), seed 1
+    want = device_scores(e, codes, offsets)
+    pc = msv.pinned_empty(codes.size, np.uint8)
+    pc[:] = codes
+    out = msv.pinned_empty(len(want), np.float32)
+    assert np.array_equal(bits(e.score_batch(codes=pc, offsets=offsets, out=out)), bits(want))
+    pc[int(offsets[4321]) + 37] = 25  # bad residue, inside the sequence's first superblock but one
+    with pytest.raises(IndexError):
+        e.score_batch(codes=pc, offsets=offsets, out=out)
+    pc[int(offsets[4321]) + 37] = codes[int(offsets[4321]) + 37]
+    assert np.array_equal(bits(e.score_batch(codes=pc, offsets=offsets, out=out)), bits(want))
+    e.close()
+
+
 def test_zero_copy_pinned_residues():
     """Page-locked residues are read by the kernel in place (no H2D): bitwise equal to the copy
     pipeline (zero-copy switched off) and to a device launch -- for a > 4 Mi-residue batch (one launch
