@@ -856,8 +856,6 @@ msv_status msv_debug_time_next_launch(msv_profile* p, void* start, void* stop) {
     return MSV_OK;
 }
 
-// Diagnostics (not in msv.h): msv_score_batch reads page-locked residues in place (1, default) or
-// copies them through the piece pipeline like pageable ones (0).
 // Diagnostics (not in msv.h): batches up to n sequences take the cooperative plan (tools/coop_sweep.py;
 // 0 turns it off).  Returns MSV_ERR_UNSUPPORTED_MODEL when the profile has no cooperative plan.
 msv_status msv_debug_set_coop_max_n(msv_profile* p, uint64_t n) {
@@ -867,8 +865,9 @@ msv_status msv_debug_set_coop_max_n(msv_profile* p, uint64_t n) {
     return MSV_OK;
 }
 
-// on: 0 = page-locked residues are copied (pipeline), 1 = read in place, 2 = read in place but without the
-// wide-block twins (A/B of the 64-byte superblock requests against the 16-byte block requests).
+// Diagnostics (not in msv.h): how msv_score_batch treats page-locked residues.  on: 0 = copied (pipeline),
+// 1 = read in place, 2 = read in place but without the wide-block twins (A/B of the 64-byte superblock
+// requests against the 16-byte block requests).
 msv_status msv_debug_set_zero_copy(msv_profile* p, int on) {
     if (!p || on < 0 || on > 2) return MSV_ERR_INVALID_ARGUMENT;
     p->zero_copy = on != 0;
