@@ -39,6 +39,10 @@ constexpr int kWords = kErrWord + 1 + kAsyncSlots + 1;
 constexpr uint64_t kChunkBytes = (1ull << 32) - (1ull << 20);
 // Host batches of at least this many residues are scored as a copy/compute pipeline of pieces.
 constexpr uint64_t kPipelineMin = 4ull << 20;
+// Small host calls (pageable residues of at most kSmallCall bytes, at most kSmallCall sequences -- the
+// reference's one-sequence-per-call pattern): residues staged behind the offsets in the pinned offsets
+// buffer and sent in ONE H2D; pageable scores written by the kernel into pinned staging (no D2H).
+constexpr uint64_t kSmallCall = 1ull << 20;
 
 struct DeviceGuard {
     int prev = -1;
@@ -276,6 +280,8 @@ struct msv_profile {
     std::vector<hipEvent_t> events;
     uint64_t* h_off = nullptr;
     size_t h_off_cap = 0;
+    float* h_sc = nullptr;  // pinned score staging of small calls with pageable destinations
+    size_t h_sc_cap = 0;
     uint32_t pipe_first_den = 4, pipe_growth = 2;  // piece sizes: total / first_den, then x growth
     uint32_t pipe_streams = 2;                      // compute streams the pieces alternate over
     bool zero_copy = true;  // page-locked residues read in place (msv_debug_set_zero_copy turns it off)
@@ -697,6 +703,7 @@ void msv_profile_destroy(msv_profile* p) {
     (void)hipFree(p->d_scores);
     (void)hipFree(p->d_order);
     if (p->h_off) (void)hipHostFree(p->h_off);
+    if (p->h_sc) (void)hipHostFree(p->h_sc);
     if (p->done) (void)hipEventDestroy(p->done);
     for (hipEvent_t e : p->events) (void)hipEventDestroy(e);
     p->kernels.destroy();
@@ -1129,21 +1136,42 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     const uint8_t* const zres = (total && p->zero_copy) ? mapped_host(residues) : nullptr;
     const std::vector<uint64_t> cut = plan_pieces(offsets, n, total, zres ? 0 : p->pipe_first_den, p->pipe_growth);
     const size_t P = cut.size() - 1;
-    if (!zres) MSV_HIP(ensure(p->d_res, p->d_res_cap, std::max<uint64_t>(total, 1)));
-    MSV_HIP(ensure(p->d_off, p->d_off_cap, n + P));
+    // SMALL calls: the residues ride in the offsets' H2D (behind the n + 1 offsets, in u64 words), and
+    // pageable scores are written by the kernel into pinned staging.  A one-sequence call was two H2D
+    // and two D2H blits, the scores' D2H to pageable memory a ~25 us round trip on the host
+    // (profiles/r03_reference_call_timeline.txt).
+    const bool small = !zres && total <= kSmallCall && n <= kSmallCall;
+    const uint64_t res_words = small ? (total + 7) / 8 : 0;
+    if (!zres && !small) MSV_HIP(ensure(p->d_res, p->d_res_cap, std::max<uint64_t>(total, 1)));
+    MSV_HIP(ensure(p->d_off, p->d_off_cap, n + P + res_words));
     // a page-locked destination is written by the kernels themselves (no D2H of the scores)
-    float* const direct = mapped_host(scores);
+    float* direct = mapped_host(scores);
+    const bool staged_scores = !direct && small;
+    if (staged_scores) {
+        if (p->h_sc_cap < n) {
+            if (p->h_sc) (void)hipHostFree(p->h_sc);
+            p->h_sc = nullptr;
+            p->h_sc_cap = 0;
+            MSV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p->h_sc), std::max<uint64_t>(n, 64) * sizeof(float),
+                                  hipHostMallocDefault));
+            p->h_sc_cap = std::max<uint64_t>(n, 64);
+        }
+        direct = mapped_host(p->h_sc);
+        if (!direct) return MSV_ERR_HIP;
+    }
     if (!direct) MSV_HIP(ensure(p->d_scores, p->d_scores_cap, n));
     float* const dsc = direct ? direct : p->d_scores;
     MSV_HIP(ensure(p->d_order, p->d_order_cap, n));
-    if (p->h_off_cap < n + P + 8) {  // pinned, so the offsets H2D is a true async DMA (+ the error word)
+    if (p->h_off_cap < n + P + 8 + res_words) {  // pinned: the offsets H2D is a true async DMA (+ the error word)
         if (p->h_off) (void)hipHostFree(p->h_off);
         p->h_off = nullptr;
         p->h_off_cap = 0;
-        MSV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p->h_off), (n + P + 8) * sizeof(uint64_t), hipHostMallocDefault));
-        p->h_off_cap = n + P + 8;
+        MSV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p->h_off), (n + P + 8 + res_words) * sizeof(uint64_t),
+                              hipHostMallocDefault));
+        p->h_off_cap = n + P + 8 + res_words;
     }
-    uint32_t* h_err = reinterpret_cast<uint32_t*>(p->h_off + n + P);
+    uint32_t* h_err = reinterpret_cast<uint32_t*>(p->h_off + n + P + res_words);
+    const uint8_t* const d_small_res = reinterpret_cast<const uint8_t*>(p->d_off + n + P);  // SMALL: residues
     const bool pipe = P > 1 && !zres;
     hipStream_t cs[2] = {st, st}, cp = st;
     // On an early error return, copies reading the pinned h_off (rewritten by the next call) and
@@ -1178,7 +1206,7 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     const uint64_t base0 = offsets[0];
     for (size_t k = 0; k < P; ++k) {
         const uint64_t lo = offsets[cut[k]] - base0, bytes = offsets[cut[k + 1]] - offsets[cut[k]];
-        if (bytes && !zres)
+        if (bytes && !zres && !small)
             MSV_HIP(hipMemcpyAsync(p->d_res + lo, residues + base0 + lo, bytes, hipMemcpyHostToDevice, cp));
         if (pipe) MSV_HIP(hipEventRecord(p->events[2 + k], cp));  // piece k's residues landed
     }
@@ -1191,7 +1219,8 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         const uint64_t base = offsets[cut[k]], cn = cut[k + 1] - cut[k];
         for (uint64_t i = 0; i <= cn; ++i) ho[i] = offsets[cut[k] + i] - base;
     }
-    MSV_HIP(hipMemcpyAsync(p->d_off, p->h_off, (n + P) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    if (small && total) std::memcpy(p->h_off + n + P, residues + base0, total);
+    MSV_HIP(hipMemcpyAsync(p->d_off, p->h_off, (n + P + res_words) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     const bool sort = pipe || !order_needless(p, n, zres != nullptr);
     for (size_t k = 0; k < P && sort; ++k) {
         s = msv_order_longest_first(p, p->d_off + cut[k] + k, cut[k + 1] - cut[k], p->d_order + cut[k], st);
@@ -1207,7 +1236,7 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         const uint64_t lo = offsets[cut[k]] - base0, bytes = offsets[cut[k + 1]] - offsets[cut[k]];
         hipStream_t c = cs[(P - 1 - k) & 1];
         if (pipe) MSV_HIP(hipStreamWaitEvent(c, p->events[2 + k], 0));
-        const uint8_t* src = zres ? zres + base0 + lo : p->d_res + lo;
+        const uint8_t* src = zres ? zres + base0 + lo : (small ? d_small_res : p->d_res) + lo;
         s = launch_batch(p, bytes ? src : p->d_dummy, std::max<uint64_t>(bytes, 1), p->d_off + cut[k] + k,
                          cut[k + 1] - cut[k], sort ? p->d_order + cut[k] : nullptr, dsc + cut[k], c, !pipe, nullptr,
                          zres && bytes);
@@ -1222,9 +1251,10 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         // the error word is read only on that rare path (its D2H was a blit launch + 4 us per call)
         MSV_HIP(hipStreamSynchronize(st));  // also: the pinned h_off is rewritten by the next call
         drain.armed = false;
-        if (scan_scores(direct, n) == MSV_OK) return MSV_OK;
+        if (staged_scores) std::memcpy(scores, p->h_sc, n * sizeof(float));
+        if (scan_scores(scores, n) == MSV_OK) return MSV_OK;
         const msv_status e = msv_profile_check(p, st);  // reads, clears and reports the latched error bits
-        return e != MSV_OK ? e : scan_scores(direct, n);
+        return e != MSV_OK ? e : scan_scores(scores, n);
     }
     MSV_HIP(hipMemcpyAsync(scores, p->d_scores, n * sizeof(float), hipMemcpyDeviceToHost, st));
     MSV_HIP(hipMemcpyAsync(h_err, p->d_words + kErrWord, sizeof(uint32_t), hipMemcpyDeviceToHost, st));

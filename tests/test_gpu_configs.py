@@ -162,6 +162,36 @@ def test_host_pipeline_piece_edges():
     e.close()
 
 
+def test_small_host_calls_staged():
+    """Pageable host calls of at most 1 MiB of residues (msv_device.cpp kSmallCall) send the residues in
+    the offsets' H2D and take the scores through pinned staging: bitwise equal to a device launch on
+    both sides of the limit (1 MiB and 1 MiB + 1 residues), one-sequence calls of every length class,
+    an all-empty batch, and a bad residue (raises; the next call is clean)."""
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("1400.hmm")))
+    o = OracleProfile("1400")
+    rng = np.random.default_rng(97)
+    for total in (1 << 20, (1 << 20) + 1):
+        lens = np.full(total // 500, 500, np.int64)
+        lens[-1] += total - int(lens.sum())
+        codes = rng.integers(0, 20, total).astype(np.uint8)
+        offsets = np.zeros(len(lens) + 1, np.uint64)
+        offsets[1:] = np.cumsum(lens)
+        assert np.array_equal(bits(e.score_batch(codes=codes, offsets=offsets)), bits(device_scores(e, codes, offsets)))
+    for L in (0, 1, 7, 16, 17, 3500, 20_000):
+        c = rng.integers(0, 20, L).astype(np.uint8)
+        off = np.array([0, L], np.uint64)
+        assert bits(e.score_batch(codes=c, offsets=off))[0] == bits(o.score_batch(c, off))[0], L
+    assert np.all(np.isneginf(e.score_batch(codes=np.zeros(0, np.uint8), offsets=np.zeros(4, np.uint64))))
+    c = rng.integers(0, 20, 900).astype(np.uint8)
+    off = np.array([0, 300, 900], np.uint64)
+    bad = c.copy()
+    bad[450] = 20
+    with pytest.raises(IndexError):
+        e.score_batch(codes=bad, offsets=off)
+    assert np.array_equal(bits(e.score_batch(codes=c, offsets=off)), bits(o.score_batch(c, off)))
+    e.close()
+
+
 def test_one_profile_on_two_streams_without_sync():
     """launches of one profile on different streams with no synchronisation between them
     (a device call on a torch stream, then the host API on the library's stream, then two more
