@@ -277,6 +277,7 @@ struct msv_profile {
     // host-API pipeline (msv_score_batch): a second compute stream, a copy stream, piece events,
     // and pinned staging for the rebased offsets
     hipStream_t stream2 = nullptr, copy_stream = nullptr;
+    hipStream_t offsets_stream = nullptr;  // msv_score_batch_async: the offsets' H2D, beside the residues'
     std::vector<hipEvent_t> events;
     uint64_t* h_off = nullptr;
     size_t h_off_cap = 0;
@@ -302,7 +303,7 @@ struct msv_profile {
         uint32_t* h_err = nullptr;  // pinned copy of the slot's error word
         const float* direct = nullptr;  // page-locked destination written by the kernel (errors: scan)
         uint64_t n = 0;
-        hipEvent_t copied = nullptr, done = nullptr;
+        hipEvent_t copied = nullptr, done = nullptr, off_copied = nullptr;
         uint64_t ticket = 0;
         bool pending = false;
     } async[kAsyncSlots];
@@ -710,6 +711,7 @@ void msv_profile_destroy(msv_profile* p) {
     p->orders.destroy();
     for (auto& a : p->async) {
         if (a.copied) (void)hipEventDestroy(a.copied);
+        if (a.off_copied) (void)hipEventDestroy(a.off_copied);
         if (a.done) (void)hipEventDestroy(a.done);
         (void)hipFree(a.d_res);
         (void)hipFree(a.d_off);
@@ -721,6 +723,7 @@ void msv_profile_destroy(msv_profile* p) {
     if (p->stream) (void)hipStreamDestroy(p->stream);
     if (p->stream2) (void)hipStreamDestroy(p->stream2);
     if (p->copy_stream) (void)hipStreamDestroy(p->copy_stream);
+    if (p->offsets_stream) (void)hipStreamDestroy(p->offsets_stream);
     delete p;
 }
 
@@ -1284,7 +1287,9 @@ msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const 
     DeviceGuard g(p->device);
     if (!g.ok) return MSV_ERR_NO_DEVICE;
     if (!p->copy_stream) MSV_HIP(hipStreamCreateWithFlags(&p->copy_stream, hipStreamNonBlocking));
+    if (!p->offsets_stream) MSV_HIP(hipStreamCreateWithFlags(&p->offsets_stream, hipStreamNonBlocking));
     if (!a.copied) MSV_HIP(hipEventCreateWithFlags(&a.copied, hipEventDisableTiming));
+    if (!a.off_copied) MSV_HIP(hipEventCreateWithFlags(&a.off_copied, hipEventDisableTiming));
     if (!a.done) MSV_HIP(hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
     if (!a.h_err) MSV_HIP(hipHostMalloc(reinterpret_cast<void**>(&a.h_err), 64, hipHostMallocDefault));
     MSV_HIP(ensure(a.d_res, a.res_cap, std::max<uint64_t>(total, 1)));
@@ -1307,21 +1312,26 @@ msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const 
     // previous call's drain tail frees instead of starting after the whole previous kernel.
     const bool odd = (p->next_ticket & 1) != 0;
     if (odd && !p->stream2) MSV_HIP(hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking));
-    hipStream_t cp = p->copy_stream, cs = odd ? p->stream2 : p->stream;
-    // copy stream: this call's inputs (they overlap the earlier calls' kernels on the compute streams).
-    // Nothing but copies goes on it: a kernel there (the order, as in round 2) waits for the running MSV
-    // grid to drain before it can start, and every later call's copies queued behind it.
-    MSV_HIP(hipMemcpyAsync(a.d_off, a.h_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, cp));
+    hipStream_t cp = p->copy_stream, co = p->offsets_stream, cs = odd ? p->stream2 : p->stream;
+    // copy streams: this call's inputs (they overlap the earlier calls' kernels on the compute streams).
+    // Nothing but copies goes on them: a kernel there (the order, as in round 2) waits for the running MSV
+    // grid to drain before it can start, and every later call's copies queued behind it.  The offsets
+    // have a stream of their own, so the copy stream carries the residues back to back (cfg2: 83 us
+    // each, which set the call rate with the offsets' 8 us copy and the gaps between them in the same
+    // stream -- profiles/r03_cfg2_streamed_timeline.txt) and the order starts once the offsets land.
+    MSV_HIP(hipMemcpyAsync(a.d_off, a.h_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, co));
+    MSV_HIP(hipEventRecord(a.off_copied, co));
     if (total) MSV_HIP(hipMemcpyAsync(a.d_res, residues + base, total, hipMemcpyHostToDevice, cp));
     MSV_HIP(hipEventRecord(a.copied, cp));
     // compute stream: order, kernel, scores and the slot's error word back to the host (the order runs
     // in the previous call's drain tail: that call's kernel is on the other compute stream)
-    MSV_HIP(hipStreamWaitEvent(cs, a.copied, 0));
+    MSV_HIP(hipStreamWaitEvent(cs, a.off_copied, 0));
     const bool sort = n && !order_needless(p, n, false);
     if (sort) {
         s = msv_order_longest_first(p, a.d_off, n, a.d_ord, cs);
         if (s != MSV_OK) return s;
     }
+    MSV_HIP(hipStreamWaitEvent(cs, a.copied, 0));
     if (n) {
         s = launch_batch(p, total ? a.d_res : p->d_dummy, std::max<uint64_t>(total, 1), a.d_off, n,
                          sort ? a.d_ord : nullptr, direct ? direct : a.d_sc, cs, true, d_err);
