@@ -4,6 +4,7 @@ against the 16-byte blocks of the ordinary variant (mode 2), interleaved over ro
 launch of the same batch for the fraction.  One JSON line per (shape, mode, round).
 
     python3 tools/zc_wide_ab.py --rounds 3
+    python3 tools/zc_wide_ab.py --modes 1,0 --shapes 100.hmm:10000,1400.hmm:100000   (in place vs copied)
 """
 from __future__ import annotations
 
@@ -25,7 +26,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--calls", type=int, default=50)
+    ap.add_argument("--modes", default="1,2", help="msv_debug_set_zero_copy modes: 1 wide twin, 2 16-B blocks, 0 copied")
+    ap.add_argument("--shapes", default="", help="profile:n,... (lengths U[300,500]); default: SHAPES")
     a = ap.parse_args()
+    modes = [int(x) for x in a.modes.split(",")]
+    shapes = SHAPES if not a.shapes else [(x.split(":")[0], int(x.split(":")[1]), 300, 500, k + 1)
+                                          for k, x in enumerate(a.shapes.split(","))]
     import numpy as np
     import torch
     import bench  # noqa: F401  (sets GPU_MAX_HW_QUEUES before HIP starts)
@@ -34,7 +40,7 @@ def main():
     from hmm_fasta_viterbi_amd.synthetic import random_batch
     L = _native.lib()
     L.msv_debug_set_zero_copy.argtypes = [C.c_void_p, C.c_int]
-    for prof, n, lo, hi, seed in SHAPES:
+    for prof, n, lo, hi, seed in shapes:
         e = msv.MSV_HMM(msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof)))
         codes, offsets = random_batch(seed, n, lo, hi)
         pc = msv.pinned_empty(codes.size, np.uint8)
@@ -53,8 +59,8 @@ def main():
 
         ref = None
         for rnd in range(a.rounds):
-            for mode in (1, 2, 0):
-                if mode == 0:
+            for mode in ["resident"] + modes:
+                if mode == "resident":
                     for _ in range(5):
                         resident()
                     st.synchronize()
@@ -77,7 +83,7 @@ def main():
                     ref = got
                 same = bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32)))
                 print(json.dumps({"profile": prof, "n": n, "len": [lo, hi], "round": rnd,
-                                  "mode": {0: "resident", 1: "pinned_wide", 2: "pinned_16B"}[mode],
+                                  "mode": mode if mode == "resident" else {0: "pinned_copy", 1: "pinned_wide", 2: "pinned_16B"}[mode],
                                   "ms_per_call": round(ms, 4), "variant": e.variant_for(n), "bitwise_same": same}),
                       flush=True)
         assert L.msv_debug_set_zero_copy(e._p, 1) == 0
