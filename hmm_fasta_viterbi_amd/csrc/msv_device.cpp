@@ -43,6 +43,10 @@ constexpr uint64_t kPipelineMin = 4ull << 20;
 // reference's one-sequence-per-call pattern): residues staged behind the offsets in the pinned offsets
 // buffer and sent in ONE H2D; pageable scores written by the kernel into pinned staging (no D2H).
 constexpr uint64_t kSmallCall = 1ull << 20;
+// Page-locked residues are read in place unless the model has fewer than kInPlaceMinStates states and the
+// batch at least kInPlaceAnyBytes residues (msv_score_batch).
+constexpr uint32_t kInPlaceMinStates = 300;
+constexpr uint64_t kInPlaceAnyBytes = 16ull << 20;
 
 struct DeviceGuard {
     int prev = -1;
@@ -1136,7 +1140,12 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     // 2.87 ms from HBM -- 0.96 of the resident rate with no copy, against ~0.85 for the copy pipeline
     // below, whose first piece's copy and extra drain tail it saves (profiles/r02_zero_copy_probe.jsonl).
     // One launch per < 2^32-byte piece; no copy stream, no second compute stream.
-    const uint8_t* const zres = (total && p->zero_copy) ? mapped_host(residues) : nullptr;
+    // Except for large batches of small models, whose kernel consumes residues faster than the ~25 GB/s at
+    // which a kernel reads host memory: page-locked 100k x U[300,500] batches, per call in place vs copied
+    // (profiles/r03_ab_in_place_vs_copied.jsonl): 100.hmm 1.60 vs 1.24 ms, 200.hmm 1.69 vs 1.46, 400.hmm
+    // 1.68 vs 1.76, 600.hmm 1.75 vs 2.33, 1400.hmm 3.09 vs 3.36; 100.hmm x 20k (8 MB) 0.41 vs 0.44.
+    const bool in_place_wins = p->model_length - 1 >= kInPlaceMinStates || total < kInPlaceAnyBytes;
+    const uint8_t* const zres = (total && p->zero_copy && in_place_wins) ? mapped_host(residues) : nullptr;
     const std::vector<uint64_t> cut = plan_pieces(offsets, n, total, zres ? 0 : p->pipe_first_den, p->pipe_growth);
     const size_t P = cut.size() - 1;
     // SMALL calls: the residues ride in the offsets' H2D (behind the n + 1 offsets, in u64 words), and

@@ -162,6 +162,24 @@ def test_host_pipeline_piece_edges():
     e.close()
 
 
+def test_pinned_small_model_large_batch_copied():
+    """Page-locked residues of a small model's large batch (< 300 states, >= 16 MiB: msv_device.cpp
+    kInPlaceMinStates) are copied through the piece pipeline instead of read in place: bitwise equal to a
+    device launch, with pageable and page-locked score destinations, and to the oracle on a sample."""
+    e = msv.MSV_HMM(msv.Profile_HMM(profile_path("200.hmm")))
+    codes, offsets = random_batch(98, 50_000, 300, 500)
+    assert int(offsets[-1]) >= 16 << 20
+    want = device_scores(e, codes, offsets)
+    pc = msv.pinned_empty(codes.size, np.uint8)
+    pc[:] = codes
+    out = msv.pinned_empty(len(want), np.float32)
+    assert np.array_equal(bits(e.score_batch(codes=pc, offsets=offsets)), bits(want))
+    assert np.array_equal(bits(e.score_batch(codes=pc, offsets=offsets, out=out)), bits(want))
+    idx = sample_with_extremes(offsets, 200, 99)
+    assert np.array_equal(bits(want[idx]), bits(OracleProfile("200").score_batch(*subset(codes, offsets, idx))))
+    e.close()
+
+
 def test_small_host_calls_staged():
     """Pageable host calls of at most 1 MiB of residues (msv_device.cpp kSmallCall) send the residues in
     the offsets' H2D and take the scores through pinned staging: bitwise equal to a device launch on
