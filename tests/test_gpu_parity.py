@@ -968,3 +968,48 @@ def test_coop_plan_device_order_async_and_shards():
     for x in engines:
         x.close()
     e.close()
+
+
+@pytest.mark.parametrize("prof", PROFILES)
+def test_every_plan_of_every_profile(prof):
+    """Every kernel plan a profile installs (cooperative, latency, mid, throughput -- msv_profile_describe),
+    each at the largest batch that takes it and the main plan beyond them, as HBM-resident launches with
+    the longest-first order: the plan named by variant_for(n) runs, and its scores equal the oracle on a
+    sample of each batch that includes the longest and shortest sequences (lengths U[0,700])."""
+    import torch
+    e = engine(prof)
+    info = e.describe()
+    sizes = {1}
+    for key in ("coop_max_n", "latency_max_n", "mid_max_n"):
+        if info[key]:
+            sizes.add(int(info[key]))
+    sizes.add(max(sizes) + 2000)
+    o = OracleProfile(prof)
+    dev = torch.device("cuda:0")
+    st = torch.cuda.Stream(dev)
+    names = {info["coop_variant"], info["latency_variant"], info["mid_variant"], info["variant"]} - {""}
+    ran = set()
+    for k, n in enumerate(sorted(sizes)):
+        codes, offsets = random_batch(7000 + 31 * k + int(prof.split(".")[0]), n, 0, 700)
+        ran.add(e.variant_for(n))
+        r = torch.from_numpy(codes).to(dev)
+        off = torch.from_numpy(offsets.view(np.int64)).to(dev)
+        s = torch.full((n,), float("nan"), dtype=torch.float32, device=dev)
+        order = torch.empty(n, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        e.order_longest_first(off.data_ptr(), n, order.data_ptr(), st.cuda_stream)
+        e.score_batch_device(r.data_ptr(), r.numel(), off.data_ptr(), n, s.data_ptr(), order.data_ptr(), st.cuda_stream)
+        e.check(st.cuda_stream)
+        got = s.cpu().numpy()
+        lens = np.diff(offsets.astype(np.int64))
+        rng = np.random.default_rng(n)
+        idx = np.unique(np.concatenate([[int(np.argmax(lens)), int(np.argmin(lens)), 0, n - 1],
+                                        rng.choice(n, min(n, 150), replace=False)]))
+        parts = [codes[int(offsets[i]):int(offsets[i + 1])] for i in idx]
+        so = np.zeros(len(idx) + 1, np.uint64)
+        so[1:] = np.cumsum([len(p) for p in parts])
+        sc = np.concatenate(parts) if so[-1] else np.zeros(0, np.uint8)
+        want = o.score_batch(sc, so, threads=min(16, len(os.sched_getaffinity(0))))
+        assert np.array_equal(bits(got[idx]), bits(want)), (prof, n, e.variant_for(n))
+    assert ran <= names and info["variant"] in ran, (prof, ran, names)
+    assert not info["coop_max_n"] or info["coop_variant"] in ran
