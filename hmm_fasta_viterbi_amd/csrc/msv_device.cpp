@@ -1322,6 +1322,16 @@ msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const 
     const bool odd = (p->next_ticket & 1) != 0;
     if (odd && !p->stream2) MSV_HIP(hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking));
     hipStream_t cp = p->copy_stream, co = p->offsets_stream, cs = odd ? p->stream2 : p->stream;
+    // On an error return after the first enqueue, copies reading this slot's pinned offsets (rewritten by
+    // the slot's next call) may still be queued: drain the call's streams first.
+    struct Drain {
+        hipStream_t s[3];
+        bool armed = true;
+        ~Drain() {
+            if (armed)
+                for (hipStream_t x : s) (void)hipStreamSynchronize(x);
+        }
+    } drain{{co, cp, cs}};
     // copy streams: this call's inputs (they overlap the earlier calls' kernels on the compute streams).
     // Nothing but copies goes on them: a kernel there (the order, as in round 2) waits for the running MSV
     // grid to drain before it can start, and every later call's copies queued behind it.  The offsets
@@ -1352,6 +1362,7 @@ msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const 
         MSV_HIP(hipMemsetAsync(d_err, 0, sizeof(uint32_t), cs));
     }
     MSV_HIP(hipEventRecord(a.done, cs));
+    drain.armed = false;
     a.direct = direct ? scores : nullptr;
     a.n = n;
     a.ticket = p->next_ticket++;
