@@ -1033,6 +1033,12 @@ msv_status msv_score_batch_device(msv_profile* p, const uint8_t* d_residues, uin
     return launch_batch(p, d_residues, residues_len, d_offsets, n, d_order, d_scores, stream, true);
 }
 
+// Library-internal (msv_score_batch, msv_multi.cpp): whether page-locked residues of `bytes` bytes are read
+// in place (zero-copy) rather than copied -- see msv_score_batch.
+__attribute__((visibility("hidden"))) bool msv_in_place_wins(const msv_profile* p, uint64_t bytes) {
+    return p->model_length - 1 >= kInPlaceMinStates || bytes < kInPlaceAnyBytes;
+}
+
 // Library-internal (msv_multi.cpp): msv_score_batch_device for residues that are the device alias of
 // page-locked host memory -- the launch takes the variant's zero-copy twin (msv_kernel.hip zc_fn).
 __attribute__((visibility("hidden"))) msv_status msv_score_batch_host_residues(
@@ -1144,7 +1150,7 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
     // which a kernel reads host memory: page-locked 100k x U[300,500] batches, per call in place vs copied
     // (profiles/r03_ab_in_place_vs_copied.jsonl): 100.hmm 1.60 vs 1.24 ms, 200.hmm 1.69 vs 1.46, 400.hmm
     // 1.68 vs 1.76, 600.hmm 1.75 vs 2.33, 1400.hmm 3.09 vs 3.36; 100.hmm x 20k (8 MB) 0.41 vs 0.44.
-    const bool in_place_wins = p->model_length - 1 >= kInPlaceMinStates || total < kInPlaceAnyBytes;
+    const bool in_place_wins = msv_in_place_wins(p, total);
     const uint8_t* const zres = (total && p->zero_copy && in_place_wins) ? mapped_host(residues) : nullptr;
     const std::vector<uint64_t> cut = plan_pieces(offsets, n, total, zres ? 0 : p->pipe_first_den, p->pipe_growth);
     const size_t P = cut.size() - 1;

@@ -19,6 +19,8 @@
 
 #include "msv.h"
 
+// msv_device.cpp (library-internal): whether page-locked residues are read in place for this model and size.
+extern "C" bool msv_in_place_wins(const msv_profile* p, uint64_t bytes);
 // msv_device.cpp (library-internal): msv_score_batch_device for page-locked host residues (zero-copy twin).
 extern "C" msv_status msv_score_batch_host_residues(msv_profile* p, const uint8_t* d_residues, uint64_t residues_len,
                                          const uint64_t* d_offsets, uint64_t n, const uint32_t* d_order,
@@ -119,7 +121,9 @@ msv_status enqueue_shard(Rank& r, const uint8_t* residues, const uint64_t* offse
     if (!g.ok) return MSV_ERR_NO_DEVICE;
     const uint64_t cn = last - first;
     MM_HIP(grow(r.d_sc, r.sc_cap, cn));
-    const uint8_t* const zres = pinned_alias(residues);
+    // (copied instead where the kernel would outrun the in-place reads: small models, large shards)
+    const uint8_t* const zres =
+        msv_in_place_wins(r.profile, offsets[last] - offsets[first]) ? pinned_alias(residues) : nullptr;
     uint64_t a = first;
     while (a < last) {  // chunks addressing < kChunkBytes residues each
         uint64_t b = a + 1;

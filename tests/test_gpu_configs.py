@@ -175,6 +175,10 @@ def test_pinned_small_model_large_batch_copied():
     out = msv.pinned_empty(len(want), np.float32)
     assert np.array_equal(bits(e.score_batch(codes=pc, offsets=offsets)), bits(want))
     assert np.array_equal(bits(e.score_batch(codes=pc, offsets=offsets, out=out)), bits(want))
+    shards = [msv.MSV_HMM(msv.Profile_HMM(profile_path("200.hmm")), device=0) for _ in range(2)]
+    assert np.array_equal(bits(msv.score_batch_multi(shards, codes=pc, offsets=offsets)), bits(want))  # same policy
+    for x in shards:
+        x.close()
     idx = sample_with_extremes(offsets, 200, 99)
     assert np.array_equal(bits(want[idx]), bits(OracleProfile("200").score_batch(*subset(codes, offsets, idx))))
     e.close()
