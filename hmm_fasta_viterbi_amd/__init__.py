@@ -7,6 +7,9 @@ Python mirror of the reference's C++ class surface, bound to libmsv_hip.so (incl
     MSV_HMM(profile).run_on_sequence(seq)   algorithms/MSV_HMM.hpp:17-44
                     .parallel_run_on_sequence(seq, should_specialize=False)
                     .score_batch(...)       (new: one fused kernel launch per batch)
+    Viterbi_HMM(profile)                    (new, SURVEY 8(f)-4: the Viterbi stage over the parse the
+                                             reference never scores with, Profile_HMM.cpp:107-120)
+    filter_pipeline(msv, vit, ...)          MSV -> P-value -> F1 -> Viterbi on the survivors, on the GPU
 
 Sequences use the reference's form ('#' sentinel + one-letter residues) or packed codes
 0..19 (alphabetical A C D E F G H I K L M N P Q R S T V W Y) with CSR offsets.
@@ -25,8 +28,12 @@ from ._native import MSVError, check
 __all__ = [
     "AMINO_ACIDS", "MSVError", "Profile_HMM", "FASTA_protein_sequences", "MSV_HMM", "pack_sequences",
     "encode", "sequence_transitions", "device_count", "score_grid", "score_grid_device", "score_batch_multi",
-    "shard_bounds", "FASTA_device", "MultiGPU",
+    "shard_bounds", "FASTA_device", "MultiGPU", "Viterbi_HMM", "filter_pipeline", "INSERTS_ZERO",
+    "INSERTS_LOG_ODDS",
 ]
+
+INSERTS_ZERO = 0      # HMMER3's insert scores (background emissions: 0)
+INSERTS_LOG_ODDS = 1  # logf(insert_emissions / background) of the reference's parse
 
 AMINO_ACIDS = "ACDEFGHIKLMNPQRSTVWY"  # MSV_HMM.cpp:29-31
 _LUT = np.full(256, 254, np.uint8)
@@ -333,6 +340,146 @@ class MSV_HMM:
 
     def __del__(self):
         self.close()
+
+
+class Viterbi_HMM:
+    """Viterbi stage for one profile on one GPU: HMMER3's generic local Viterbi over the
+    reference's parse (insert emissions, 7 transitions per node: Profile_HMM.cpp:107-120) with the MSV
+    path's specials (MSV_HMM.cpp:49-64); msv.h states the recurrence.  Every score comes from the gfx950
+    kernel (vit_kernel.hip) except run_on_sequence, which -- like the reference's MSV run_on_sequence --
+    is the library's serial CPU DP.  P-values use STATS LOCAL VITERBI (Profile_HMM.cpp:86-87)."""
+
+    def __init__(self, base_hmm: Profile_HMM, device: int = 0, insert_mode: int = INSERTS_ZERO):
+        L = _native.lib()
+        M = base_hmm.model_length
+        self.model_length = M
+        self.insert_mode = insert_mode
+        self.match_scores = np.zeros((20, M), np.float32)
+        self.insert_scores = np.zeros((20, M), np.float32)
+        self.transition_scores = np.zeros((M, 7), np.float32)
+        b, c, j = C.c_float(), C.c_float(), C.c_float()
+        check(L.msv_hmm_viterbi_scores(base_hmm._h, insert_mode, self.match_scores.ctypes.data,
+                                       self.insert_scores.ctypes.data, self.transition_scores.ctypes.data,
+                                       C.byref(b), C.byref(c), C.byref(j)), "msv_hmm_viterbi_scores")
+        self.tr_B_Mk, self.tr_E_C, self.tr_E_J = b.value, c.value, j.value
+        p = C.c_void_p()
+        check(L.msv_vit_profile_create(device, self.match_scores.ctypes.data,
+                                       self.insert_scores.ctypes.data if insert_mode == INSERTS_LOG_ODDS else None,
+                                       self.transition_scores.ctypes.data, M, self.tr_B_Mk, self.tr_E_C, self.tr_E_J,
+                                       C.byref(p)), "msv_vit_profile_create")
+        self._p = p
+        self.device = device
+        self.viterbi_mu = base_hmm.stats_local_viterbi_mu
+        self.viterbi_lambda = base_hmm.stats_local_viterbi_lambda
+
+    def run_on_sequence(self, seq: str) -> float:
+        """The serial CPU Viterbi (msv_vit_cpu_score); IndexError on a residue outside the 20."""
+        codes = encode(seq[1:] if seq.startswith("#") else seq)
+        out = C.c_float()
+        st = _native.lib().msv_vit_cpu_score(
+            self.match_scores.ctypes.data, self.insert_scores.ctypes.data if self.insert_mode else None,
+            self.transition_scores.ctypes.data, self.model_length, self.tr_B_Mk, self.tr_E_C, self.tr_E_J,
+            codes.ctypes.data if codes.size else None, codes.size, C.byref(out))
+        check(st, "msv_vit_cpu_score")
+        return out.value
+
+    def parallel_run_on_sequence(self, seq: str) -> float:
+        return float(self.score_batch([seq])[0])
+
+    def score_batch(self, seqs: Sequence[str] | None = None, *, codes: np.ndarray | None = None,
+                    offsets: np.ndarray | None = None) -> np.ndarray:
+        """Viterbi scores of every sequence of a host batch (msv_vit_score_batch, one launch)."""
+        if seqs is not None:
+            codes, offsets = pack_sequences(seqs)
+        codes = np.ascontiguousarray(codes, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        n = len(offsets) - 1
+        out = np.zeros(n, np.float32)
+        st = _native.lib().msv_vit_score_batch(self._p, codes.ctypes.data if codes.size else None,
+                                               offsets.ctypes.data, n, out.ctypes.data, None)
+        if st == _native.MSV_ERR_BAD_RESIDUE:
+            raise IndexError("residue outside the 20 amino acids")
+        check(st, "msv_vit_score_batch")
+        return out
+
+    def score_batch_device(self, residues_ptr: int, residues_len: int, offsets_ptr: int, n: int, scores_ptr: int,
+                           select_ptr: int | None = None, select_count_ptr: int | None = None,
+                           stream: int | None = None) -> None:
+        """Device-resident batch (raw device pointers), optionally only the sequences listed at select_ptr
+        (uint32; their count in the device uint32 at select_count_ptr, else n); async on `stream`."""
+        check(_native.lib().msv_vit_score_batch_device(self._p, residues_ptr, residues_len, offsets_ptr, n,
+                                                       select_ptr, select_count_ptr, scores_ptr, stream),
+              "msv_vit_score_batch_device")
+
+    def reserve_length(self, max_length: int) -> None:
+        check(_native.lib().msv_vit_profile_reserve_length(self._p, max_length))
+
+    def check(self, stream: int | None = None) -> None:
+        st = _native.lib().msv_vit_profile_check(self._p, stream)
+        if st == _native.MSV_ERR_BAD_RESIDUE:
+            raise IndexError("residue outside the 20 amino acids")
+        check(st, "msv_vit_profile_check")
+
+    def pvalues(self, scores: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+        """P-values of Viterbi scores against STATS LOCAL VITERBI (HMMER3's formula, msv_pvalues)."""
+        scores = np.ascontiguousarray(scores, np.float32)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        n = len(offsets) - 1
+        if scores.shape != (n,):
+            raise ValueError("scores and offsets disagree")
+        out = np.zeros(n, np.float64)
+        check(_native.lib().msv_pvalues(scores.ctypes.data, offsets.ctypes.data, n, self.viterbi_mu,
+                                        self.viterbi_lambda, out.ctypes.data), "msv_pvalues")
+        return out
+
+    def set_variant(self, name: str) -> None:
+        check(_native.lib().msv_vit_profile_set_variant(self._p, name.encode()), f"set_variant({name})")
+
+    @staticmethod
+    def variants() -> list[str]:
+        L = _native.lib()
+        return [L.msv_vit_variant_name(i).decode() for i in range(L.msv_vit_variant_count())]
+
+    def describe(self) -> dict:
+        info = _native.VitInfo()
+        check(_native.lib().msv_vit_profile_describe(self._p, C.byref(info)))
+        return info.as_dict()
+
+    def close(self):
+        lib = _loaded_lib()
+        if getattr(self, "_p", None) and lib is not None:
+            lib.msv_vit_profile_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.close()
+
+
+def filter_pipeline(msv_engine: MSV_HMM, vit_engine: Viterbi_HMM, seqs: Sequence[str] | None = None, *,
+                    codes: np.ndarray | None = None, offsets: np.ndarray | None = None, F1: float = 0.02):
+    """HMMER3's MSV -> Viterbi cascade on the GPU (msv_vit_filter_batch): MSV scores of every sequence,
+    the survivors P <= F1 (STATS LOCAL MSV), their Viterbi scores (-inf elsewhere) and Viterbi P-values
+    (STATS LOCAL VITERBI, NaN elsewhere).  Returns (msv_scores, passed, vit_scores, vit_pvalues)."""
+    if seqs is not None:
+        codes, offsets = pack_sequences(seqs)
+    codes = np.ascontiguousarray(codes, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = len(offsets) - 1
+    msc = np.zeros(n, np.float32)
+    passed = np.zeros(n, np.uint8)
+    vsc = np.zeros(n, np.float32)
+    npass = C.c_uint64(0)
+    st = _native.lib().msv_vit_filter_batch(msv_engine._p, vit_engine._p, codes.ctypes.data if codes.size else None,
+                                            offsets.ctypes.data, n, msv_engine.msv_mu, msv_engine.msv_lambda, F1,
+                                            msc.ctypes.data, passed.ctypes.data, vsc.ctypes.data, C.byref(npass))
+    if st == _native.MSV_ERR_BAD_RESIDUE:
+        raise IndexError("residue outside the 20 amino acids")
+    check(st, "msv_vit_filter_batch")
+    mask = passed.astype(bool)
+    vpv = np.full(n, np.nan)
+    if mask.any():
+        vpv[mask] = vit_engine.pvalues(vsc, offsets)[mask]
+    return msc, mask, vsc, vpv
 
 
 def _handles(engines: Sequence[MSV_HMM]):

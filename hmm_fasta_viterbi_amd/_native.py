@@ -49,6 +49,10 @@ EXPORTED = [
     "msv_score_batch_async", "msv_profile_wait", "msv_profile_bind_stream",
     "msv_multi_create", "msv_multi_score_batch", "msv_multi_destroy",
     "msv_host_alloc", "msv_host_free", "msv_profile_variant_for",
+    "msv_filter_select_device", "msv_hmm_viterbi_scores", "msv_vit_cpu_score", "msv_vit_profile_create",
+    "msv_vit_profile_create_from_hmm", "msv_vit_profile_destroy", "msv_vit_profile_reserve_length",
+    "msv_vit_profile_describe", "msv_vit_variant_count", "msv_vit_variant_name", "msv_vit_profile_set_variant",
+    "msv_vit_score_batch_device", "msv_vit_score_batch", "msv_vit_profile_check", "msv_vit_filter_batch",
 ]
 
 
@@ -88,6 +92,27 @@ class KernelInfo(C.Structure):
         d["latency_variant"] = self.latency_variant.decode()
         d["mid_variant"] = self.mid_variant.decode()
         d["coop_variant"] = self.coop_variant.decode()
+        return d
+
+
+class VitInfo(C.Structure):
+    _fields_ = [
+        ("model_length", C.c_uint32),
+        ("states_per_lane", C.c_uint32),
+        ("transitions_in_registers", C.c_uint32),
+        ("match_in_lds", C.c_uint32),
+        ("insert_scores", C.c_uint32),
+        ("waves_per_block", C.c_uint32),
+        ("blocks", C.c_uint32),
+        ("lds_bytes", C.c_uint32),
+        ("max_length", C.c_uint32),
+        ("device", C.c_int),
+        ("variant", C.c_char * 64),
+    ]
+
+    def as_dict(self) -> dict:
+        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d["variant"] = self.variant.decode()
         return d
 
 
@@ -175,6 +200,22 @@ def lib() -> C.CDLL:
         "msv_score_fasta_device": (C.c_int, [vp, vp, vp]),
         "msv_score_batch_multi": (C.c_int, [vp, C.c_uint32, vp, vp, u64, vp]),
         "msv_pvalues_device": (C.c_int, [C.c_int, vp, vp, u64, C.c_float, C.c_float, vp, vp]),
+        "msv_filter_select_device": (C.c_int, [C.c_int, vp, vp, u64, f32, f32, C.c_double, vp, vp, vp, vp]),
+        "msv_hmm_viterbi_scores": (C.c_int, [vp, C.c_int, vp, vp, vp, fp, fp, fp]),
+        "msv_vit_cpu_score": (C.c_int, [vp, vp, vp, u32, f32, f32, f32, vp, u64, fp]),
+        "msv_vit_profile_create": (C.c_int, [C.c_int, vp, vp, vp, u32, f32, f32, f32, C.POINTER(vp)]),
+        "msv_vit_profile_create_from_hmm": (C.c_int, [C.c_int, vp, C.c_int, C.POINTER(vp)]),
+        "msv_vit_profile_destroy": (None, [vp]),
+        "msv_vit_profile_reserve_length": (C.c_int, [vp, u64]),
+        "msv_vit_profile_describe": (C.c_int, [vp, C.POINTER(VitInfo)]),
+        "msv_vit_variant_count": (C.c_int, []),
+        "msv_vit_variant_name": (C.c_char_p, [C.c_int]),
+        "msv_vit_profile_set_variant": (C.c_int, [vp, C.c_char_p]),
+        "msv_vit_score_batch_device": (C.c_int, [vp, vp, u64, vp, u64, vp, vp, vp, vp]),
+        "msv_vit_score_batch": (C.c_int, [vp, vp, vp, u64, vp, vp]),
+        "msv_vit_profile_check": (C.c_int, [vp, vp]),
+        "msv_vit_filter_batch": (C.c_int, [vp, vp, vp, vp, u64, f32, f32, C.c_double, vp, vp, vp,
+                                           C.POINTER(C.c_uint64)]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("MSV_LIB_PATH") and not hasattr(L, name):

@@ -59,6 +59,48 @@ msv_status msv_hmm_msv_scores(const msv_hmm* hmm, float* emission_scores, float*
     return MSV_OK;
 }
 
+msv_status msv_hmm_viterbi_scores(const msv_hmm* hmm, int insert_mode, float* match_scores, float* insert_scores,
+                                  float* transition_scores, float* tr_B_Mk, float* tr_E_C, float* tr_E_J) {
+    if (!hmm || (insert_mode != MSV_INSERTS_ZERO && insert_mode != MSV_INSERTS_LOG_ODDS))
+        return MSV_ERR_INVALID_ARGUMENT;
+    const size_t M = msv_hmm_model_length(hmm);
+    std::vector<float> msc(20 * M);
+    float b, c, j;
+    msv_status s = msv_hmm_msv_scores(hmm, msc.data(), &b, &c, &j);  // match scores and specials: the MSV path's
+    if (s != MSV_OK) return s;
+    if (match_scores) std::copy(msc.begin(), msc.end(), match_scores);
+    if (insert_scores) {
+        static constexpr float bg[20] = {0.0787945f, 0.0151600f, 0.0535222f, 0.0668298f, 0.0397062f,
+                                         0.0695071f, 0.0229198f, 0.0590092f, 0.0594422f, 0.0963728f,
+                                         0.0237718f, 0.0414386f, 0.0482904f, 0.0395639f, 0.0540978f,
+                                         0.0683364f, 0.0540687f, 0.0673417f, 0.0114135f, 0.0304133f};
+        const float* ins = msv_hmm_insert_emissions(hmm);  // Profile_HMM.cpp:113-115
+        for (size_t k = 0; k < M; ++k)
+            for (size_t r = 0; r < 20; ++r)
+                insert_scores[r * M + k] = insert_mode == MSV_INSERTS_LOG_ODDS ? std::log(ins[k * 20 + r] / bg[r]) : 0.0f;
+    }
+    if (transition_scores) {
+        const float* t = msv_hmm_transitions(hmm);  // p = exp(-x) as parsed (Profile_HMM.cpp:41, :116-119)
+        for (size_t k = 0; k < M * 7; ++k) transition_scores[k] = std::log(t[k]);
+    }
+    if (tr_B_Mk) *tr_B_Mk = b;
+    if (tr_E_C) *tr_E_C = c;
+    if (tr_E_J) *tr_E_J = j;
+    return MSV_OK;
+}
+
+msv_status msv_vit_cpu_score(const float* match_scores, const float* insert_scores, const float* transition_scores,
+                             uint32_t model_length, float tr_B_Mk, float tr_E_C, float tr_E_J, const uint8_t* codes,
+                             uint64_t L, float* score) {
+    if (!match_scores || !transition_scores || !score || model_length < 2 || (L && !codes))
+        return MSV_ERR_INVALID_ARGUMENT;
+    for (uint64_t i = 0; i < L; ++i)
+        if (codes[i] >= 20) return MSV_ERR_BAD_RESIDUE;
+    *score = msv_host::viterbi_run_on_sequence(match_scores, insert_scores, transition_scores, model_length, tr_B_Mk,
+                                               tr_E_C, tr_E_J, codes, L);
+    return MSV_OK;
+}
+
 msv_status msv_shard_bounds(const uint64_t* offsets, uint64_t n, uint32_t n_shards, uint64_t* bounds) {
     if (!bounds || n_shards == 0 || (n && !offsets)) return MSV_ERR_INVALID_ARGUMENT;
     bounds[0] = 0;
@@ -114,6 +156,53 @@ float run_on_sequence(const float* emission_scores, size_t M, float tr_B_Mk, flo
         std::swap(prev, cur);
     }
     return C + move;  // dp.back()[C] + tr_move; -inf for an empty sequence
+}
+
+float viterbi_run_on_sequence(const float* msc, const float* isc, const float* tsc, size_t M, float tr_B_Mk,
+                              float tr_E_C, float tr_E_J, const uint8_t* codes, size_t L) {
+    // The Viterbi stage's sequential DP (msv.h): HMMER3's generic local Viterbi over the reference's parse
+    // with the MSV specials.  One row of each state, updated in place from the highest node down (M(k)
+    // and I(k) read only the previous row at k-1 and k), then the row's D chain from the lowest node up.
+    // Nodes K = M - 1; transitions of node t at tsc[t * 7 + x], read for nodes 1 .. K-1 only.
+    constexpr float ninf = -std::numeric_limits<float>::infinity();
+    enum { MM, MI, MD, IM, II, DM, DD };
+    const size_t K = M - 1;
+    float loop, move;
+    msv_sequence_transitions(L, &loop, &move);
+    std::vector<float> Mv(M, ninf), Iv(M, ninf), Dv(M, ninf);  // [0]: the dummy column, -inf on every row
+    float J = ninf, C = ninf, N = 0.0f, B = move;
+    for (size_t i = 0; i < L; ++i) {
+        const size_t r = codes[i];
+        const float* ms = msc + r * M;
+        const float* is = isc ? isc + r * M : nullptr;
+        const float Bt = B + tr_B_Mk;
+        float E = ninf;
+        for (size_t k = K; k >= 1; --k) {
+            const float* tp = tsc + (k - 1) * 7;  // into node k from node k-1
+            if (k < K) {
+                const float* tk = tsc + k * 7;
+                const float iv = std::max(Mv[k] + tk[MI], Iv[k] + tk[II]);
+                Iv[k] = is ? iv + is[k] : iv;
+            } else {
+                Iv[k] = ninf;  // no insert state at node K
+            }
+            float m = Bt;
+            if (k > 1) m = std::max(std::max(Mv[k - 1] + tp[MM], Iv[k - 1] + tp[IM]), std::max(Dv[k - 1] + tp[DM], m));
+            Mv[k] = m + ms[k];
+            E = std::max(E, Mv[k]);
+        }
+        Dv[1] = ninf;  // entered from node 0, which only B leaves
+        for (size_t k = 2; k <= K; ++k) {
+            const float* tp = tsc + (k - 1) * 7;
+            Dv[k] = std::max(Mv[k - 1] + tp[MD], Dv[k - 1] + tp[DD]);
+        }
+        E = std::max(E, Dv[K]);
+        J = std::max(J + loop, E + tr_E_J);
+        C = std::max(C + loop, E + tr_E_C);
+        N = N + loop;
+        B = std::max(N + move, J + move);
+    }
+    return C + move;
 }
 
 }  // namespace msv_host

@@ -24,6 +24,19 @@ constexpr int lds_rows_for(int G, int S) {
     return (kLdsLimit / (G * S * 4)) >= kTableRows ? kTableRows : (kLdsLimit / (G * S * 4));
 }
 
+// MSV filter P-value of one score (HMMER3's MSV-stage formula, msv.h msv_pvalues): used by the P-value
+// kernel, the host path and the Viterbi stage's survivor selection (vit_kernel.hip).
+__device__ __host__ inline double msv_pvalue_of(float score, uint64_t L, float mu, float lambda) {
+    if (L == 0) return 1.0;  // empty sequence: score -inf, and L log(p1) would be 0 * -inf
+    const float p1 = static_cast<float>(L) / static_cast<float>(L + 1);
+    const float nullsc = static_cast<float>(static_cast<double>(L) * log(static_cast<double>(p1)) +
+                                            log(1.0 - static_cast<double>(p1)));
+    const float bits = (score - nullsc) / 0.69314718055994529f;
+    const double y = static_cast<double>(lambda) * (static_cast<double>(bits) - static_cast<double>(mu));
+    const double ey = -exp(-y);
+    return fabs(ey) < 5e-9 ? -ey : 1.0 - exp(ey);
+}
+
 struct KernelArgs {
     const float4* etab;        // [21][S/4][G] float4, global copy of the kernel-layout table
     const uint8_t* residues;   // CSR residue codes

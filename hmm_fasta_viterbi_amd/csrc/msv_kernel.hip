@@ -191,17 +191,6 @@ __global__ __launch_bounds__(kOrderThreads) void order_place_kernel(const uint64
 // MSV filter P-values (msv.h): one thread per sequence, HBM-bound elementwise
 // (12 B read + 8 B written per sequence).  Same float/double steps as msv_stats.cpp's host path.
 // ------------------------------------------------------------------------------------------------
-__device__ __host__ inline double msv_pvalue_of(float score, uint64_t L, float mu, float lambda) {
-    if (L == 0) return 1.0;  // empty sequence: score -inf, and L log(p1) would be 0 * -inf
-    const float p1 = static_cast<float>(L) / static_cast<float>(L + 1);
-    const float nullsc = static_cast<float>(static_cast<double>(L) * log(static_cast<double>(p1)) +
-                                            log(1.0 - static_cast<double>(p1)));
-    const float bits = (score - nullsc) / 0.69314718055994529f;
-    const double y = static_cast<double>(lambda) * (static_cast<double>(bits) - static_cast<double>(mu));
-    const double ey = -exp(-y);
-    return fabs(ey) < 5e-9 ? -ey : 1.0 - exp(ey);
-}
-
 __global__ __launch_bounds__(256) void msv_pvalues_kernel(const float* __restrict__ scores,
                                                           const uint64_t* __restrict__ offsets, uint64_t n, float mu,
                                                           float lambda, double* __restrict__ out) {

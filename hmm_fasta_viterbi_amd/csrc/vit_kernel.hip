@@ -1,0 +1,394 @@
+// vit_kernel.hip -- the Viterbi stage of SURVEY 8(f)-4 as ONE persistent gfx950 kernel per batch.
+//
+// The reference parses everything a Viterbi filter needs (insert_emissions and the 7 transitions per node,
+// data_readers/Profile_HMM.cpp:107-120; STATS LOCAL VITERBI, :86-87) and never uses it; its README
+// (README.md:2-3) names Viterbi as the point of the project.  This kernel scores HMMER3's generic local
+// Viterbi (p7_GViterbi's recurrence, multihit local mode) over that parse, with the MSV path's specials
+// (tr_B_Mk entry, E->C/J, per-length N/C/J loop/move, MSV_HMM.cpp:49-64), usually on the MSV filter's
+// survivors.  Restated serially in oracle/msv_oracle.c (oracle_vit_run_codes, test-only); parity
+// against it is bitwise.  Row i, residue r, k = 1..LENG:
+//     M(i,k) = max(M'(k-1)+tMM, I'(k-1)+tIM, D'(k-1)+tDM, B'+tBM) + msc[r][k]
+//     I(i,k) = max(M'(k)+tMI, I'(k)+tII) + isc[r][k]       (isc = 0: HMMER3's insert scores)
+//     D(i,k) = max(M(k-1)+tMD, D(k-1)+tDD)                    <- within the row: a serial chain
+//     E = max_k M(i,k);  J, C, N, B as MSV                    (D(LENG) <= E always: every t <= 0)
+// Each term is ONE float add and max is exact, so any evaluation order of the maxes gives the same bits.
+//
+// Mapping (gfx950):
+//   * one sequence per 64-lane wave (the stage sees the filter's few survivors, so a sequence gets a whole
+//     wave); lane l holds the S consecutive states l*S+1 .. l*S+S of M, I, D in VGPRs;
+//   * residues are wave-uniform: one byte per lane per 64-row block (a block ahead), v_readlane per row, so
+//     the row's control, the table row address and the bad-code check are scalar;
+//   * per row: the previous row's last M/I/D cross one lane boundary by DPP (row_bcast:15 + row_shr:1);
+//     a descending pass updates M and I in place (slot q reads the old q-1), the new last M crosses, and
+//     an ascending pass runs the lane's D chain in place;
+//   * the D chain across lanes is resolved lazily (Farrar's lazy-F): the pass starts each lane's chain
+//     from -inf, then while any lane's incoming D(k-1)+tDD beats its first D, the lanes re-run
+//     D_q = max(D_q, D_{q-1}+tDD).  Lower bounds only ever rise to the exact value and fl() is
+//     monotone, so the result is the serial chain bit for bit;
+//   * J and C are per-lane partials (as the MSV kernel), the 64-lane max taken only when some J >= N
+//     and once per sequence for C;
+//   * match scores staged in LDS ([20][S/2][64] float2: each ds_read_b64 of a wave is contiguous) and the
+//     7 transition arrays in VGPRs, or (large models) transitions in LDS and match scores from L2;
+//   * persistent grid, first sequence static, then one atomic per sequence; the counter resets itself.
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "msv_kernel_impl.h"
+#include "vit_kernel.h"
+
+namespace vitk {
+
+namespace {
+
+constexpr float NINF = -__builtin_inff();
+
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
+// Lane l-1's value into lane l (64 lanes); lane 0 keeps `old`'s lane 0, which its caller keeps at -inf
+// (the dummy column k = 0).
+__device__ __forceinline__ float shift64(float last, float old) { return msvk::shift_in<64>(last, old); }
+
+}  // namespace
+
+// One chunk (two slots) of the M/I pass: the LDS-resident transition pairs among MM, IM, DM, MI, II
+// (NM of them), the match and the insert scores.  And of the D pass: the LDS-resident MD, DD pairs.
+template <int NM>
+struct ChunkMI {
+    float2 t[NM ? NM : 1];
+    float2 e, i;
+};
+template <int ND>
+struct ChunkD {
+    float2 t[ND ? ND : 1];
+};
+
+// PD > 0: a chunk's LDS/L2 data is requested PD chunks ahead and every chunk is its own scheduling region
+// (bounds the live loads: left alone, the scheduler hoists a whole row of loads and spills).
+template <int S, int NTREG, bool ELDS, bool ISC, int WAVES, int PD>
+__global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
+    static_assert(S >= 2 && S % 2 == 0, "S must be even");
+    constexpr int C2 = S / 2;
+    constexpr int ROW2 = C2 * kLanes;                     // float2 per table row
+    constexpr int NTL = kTransitions - NTREG;             // transition arrays in LDS
+    constexpr int NM = NTREG >= MD_IN ? 0 : MD_IN - NTREG;  // ... of them used by the M/I pass
+    constexpr int ND = NTL - NM;                          // ... by the D pass
+    __shared__ float2 etab_s[ELDS ? kRows * ROW2 : 1];
+    __shared__ float2 ttab_s[NTL ? NTL * ROW2 : 1];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6;
+
+    if constexpr (ELDS)
+        for (int i = threadIdx.x; i < kRows * ROW2; i += WAVES * 64) etab_s[i] = a.etab[i];
+    if constexpr (NTL > 0)
+        for (int i = threadIdx.x; i < NTL * ROW2; i += WAVES * 64) ttab_s[i] = a.ttab[NTREG * ROW2 + i];
+    if constexpr (ELDS || NTL > 0) __syncthreads();
+
+    // transition arrays 0 .. NTREG-1 live in VGPRs for the whole launch, NTREG .. 6 in LDS (re-read every row)
+    float tr[NTREG ? NTREG : 1][S];
+    if constexpr (NTREG > 0) {
+#pragma unroll
+        for (int j = 0; j < NTREG; ++j)
+#pragma unroll
+            for (int c = 0; c < C2; ++c) {
+                const float2 t = a.ttab[(j * C2 + c) * kLanes + lane];
+                tr[j][2 * c] = t.x;
+                tr[j][2 * c + 1] = t.y;
+            }
+    }
+    // `rz` is an opaque zero renewed every row: without it the compiler hoists the loop-invariant LDS loads
+    // of the transitions out of the row loop into VGPRs (and spills them), undoing the LDS arrays.
+    uint32_t rz = 0;
+    auto tlds = [&](int j, int c) -> float2 { return ttab_s[rz + ((j - NTREG) * C2 + c) * kLanes + lane]; };
+    auto tdd = [&](int q) -> float {  // DD into slot q
+        if constexpr (NTREG == kTransitions) {
+            return tr[DD_IN][q];
+        } else {
+            const float2 t = tlds(DD_IN, q / 2);
+            return (q & 1) ? t.y : t.x;
+        }
+    };
+
+    const uint64_t total = a.select_count ? static_cast<uint64_t>(*a.select_count) : a.n;
+    const uint32_t nwaves = gridDim.x * WAVES;
+    uint32_t item = blockIdx.x * WAVES + wave;
+    while (item < total) {
+        const uint32_t s = a.select ? a.select[item] : item;
+        const uint64_t o0 = a.offsets[s];
+        const uint64_t L = a.offsets[s + 1] - o0;
+        if (L == 0) {
+            if (lane == 0) a.scores[s] = NINF;  // C_0 = -inf, as MSV_HMM.cpp:86,112
+        } else if (L >= a.lentab_n) {
+            if (lane == 0) {
+                a.scores[s] = __uint_as_float(0x7fc00000u);
+                atomicOr(a.errors, msvk::kErrTooLong);
+            }
+        } else {
+            const float2 lm = a.lentab[L];
+            const float loop = lm.x, move = lm.y;
+            float M[S], I[S], D[S];
+#pragma unroll
+            for (int q = 0; q < S; ++q) M[q] = I[q] = D[q] = NINF;
+            float J = NINF, Cp = NINF;  // per-lane partials of J and C
+            float N = 0.0f, B = move;
+            float sM = NINF, sI = NINF, sD = NINF, sMn = NINF, sDn = NINF;  // shift registers, lane 0 = -inf
+            uint32_t maxcode = 0;
+            const uint8_t* res = a.residues + o0;
+            uint32_t cur = static_cast<uint64_t>(lane) < L ? res[lane] : 0u;
+            uint32_t nxt = static_cast<uint64_t>(64 + lane) < L ? res[64 + lane] : 0u;
+            // One row (residue i).  Rows run two per loop trip: a row writes its new M into registers other
+            // than the old ones (the old M(k) is read after the new one is made), so a one-row loop copied
+            // the whole row back at its back edge (22 v_mov per row at S = 22); over two rows the values
+            // return to their registers by themselves.
+            auto row = [&](uint64_t i) {
+                const uint32_t ph = static_cast<uint32_t>(i) & 63u;
+                if (ph == 0 && i != 0) {
+                    cur = nxt;
+                    nxt = (i + 64 + lane < L) ? res[i + 64 + lane] : 0u;
+                }
+                uint32_t code = __builtin_amdgcn_readlane(cur, ph);
+                maxcode = code > maxcode ? code : maxcode;
+                code = code < 19u ? code : 19u;
+                if constexpr (NTL > 0) asm volatile("" : "+v"(rz));
+                const float Bt = B + a.tr_B_Mk;
+                const float2* er;
+                if constexpr (ELDS) er = etab_s + code * ROW2 + lane;  // (one address space per variant)
+                else er = a.etab + code * ROW2 + lane;
+                const float2* ir = a.itab + code * ROW2 + lane;
+                auto load_mi = [&](int c) {
+                    ChunkMI<NM> k;
+#pragma unroll
+                    for (int j = 0; j < NM; ++j) k.t[j] = tlds(NTREG + j, c);
+                    k.e = er[c * kLanes];
+                    if constexpr (ISC) k.i = ir[c * kLanes];
+                    return k;
+                };
+                auto load_d = [&](int c) {
+                    ChunkD<ND> k;
+#pragma unroll
+                    for (int j = 0; j < ND; ++j) k.t[j] = tlds(kTransitions - ND + j, c);
+                    return k;
+                };
+                auto Tm = [&](const ChunkMI<NM>& k, int j, int q) -> float {  // j in MM_IN .. II
+                    if (j < NTREG) return tr[j < NTREG ? j : 0][q];
+                    const float2 t = k.t[j >= NTREG ? j - NTREG : 0];
+                    return (q & 1) ? t.y : t.x;
+                };
+                auto Td = [&](const ChunkD<ND>& k, int j, int q) -> float {  // j = MD_IN or DD_IN
+                    if (j < NTREG) return tr[j < NTREG ? j : 0][q];
+                    const float2 t = k.t[j - (kTransitions - ND) >= 0 ? j - (kTransitions - ND) : 0];
+                    return (q & 1) ? t.y : t.x;
+                };
+
+                // the previous row's last states, from the lane on the left (k - 1 across the boundary)
+                sM = shift64(M[S - 1], sM);
+                sI = shift64(I[S - 1], sI);
+                sD = shift64(D[S - 1], sD);
+
+                // M/I pass, highest slot first: I(k) reads M'(k), I'(k) and M(k) reads M'(k-1), I'(k-1),
+                // D'(k-1), so every register is updated in place (no copies at the loop's back edge)
+                float E = NINF;
+                ChunkMI<NM> km[C2];
+                if constexpr (PD > 0) {
+#pragma unroll
+                    for (int c = C2 - 1; c >= 0 && c >= C2 - PD; --c) km[c] = load_mi(c);
+                }
+#pragma unroll
+                for (int c = C2 - 1; c >= 0; --c) {
+                    if constexpr (PD > 0) {
+                        if (c - PD >= 0) km[c - PD] = load_mi(c - PD);
+                    } else {
+                        km[c] = load_mi(c);
+                    }
+                    const ChunkMI<NM>& k = km[c];
+#pragma unroll
+                    for (int h = 1; h >= 0; --h) {
+                        const int q = 2 * c + h;
+                        float iv = fmaxf(M[q] + Tm(k, MI, q), I[q] + Tm(k, II, q));
+                        if constexpr (ISC) iv = iv + (h ? k.i.y : k.i.x);
+                        const float pm = q ? M[q - 1] : sM, pi = q ? I[q - 1] : sI, pd = q ? D[q - 1] : sD;
+                        const float m = fmaxf(fmaxf(pm + Tm(k, MM_IN, q), pi + Tm(k, IM_IN, q)),
+                                              fmaxf(pd + Tm(k, DM_IN, q), Bt)) +
+                                        (h ? k.e.y : k.e.x);
+                        M[q] = m;
+                        I[q] = iv;
+                        E = fmaxf(E, m);
+                    }
+                    if constexpr (PD > 0) __builtin_amdgcn_sched_barrier(0);
+                }
+                // this row's M(k-1) for each lane's first slot
+                sMn = shift64(M[S - 1], sMn);
+                // D pass, lowest slot first (the chain D(k) = max(M(k-1)+tMD, D(k-1)+tDD)), each lane's
+                // chain started from -inf; lazy-F below carries D across the lane boundaries
+                ChunkD<ND> kd[C2];
+                if constexpr (PD > 0 && ND > 0) {
+#pragma unroll
+                    for (int c = 0; c < C2 && c < PD; ++c) kd[c] = load_d(c);
+                }
+#pragma unroll
+                for (int c = 0; c < C2; ++c) {
+                    if constexpr (PD > 0 && ND > 0) {
+                        if (c + PD < C2) kd[c + PD] = load_d(c + PD);
+                    } else {
+                        kd[c] = load_d(c);
+                    }
+                    const ChunkD<ND>& k = kd[c];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int q = 2 * c + h;
+                        D[q] = q ? fmaxf(M[q - 1] + Td(k, MD_IN, q), D[q - 1] + Td(k, DD_IN, q))
+                                 : sMn + Td(k, MD_IN, 0);
+                    }
+                    if constexpr (PD > 0 && ND > 0) __builtin_amdgcn_sched_barrier(0);
+                }
+                // lazy-F: carry D across lane boundaries until no lane's first state changes
+                sDn = shift64(D[S - 1], sDn);
+                float cand = sDn + tdd(0);
+                if (__builtin_expect(wave_any(cand > D[0]), 0)) {
+                    do {
+                        D[0] = fmaxf(D[0], cand);
+#pragma unroll
+                        for (int q = 1; q < S; ++q) D[q] = fmaxf(D[q], D[q - 1] + tdd(q));
+                        sDn = shift64(D[S - 1], sDn);
+                        cand = sDn + tdd(0);
+                    } while (wave_any(cand > D[0]));
+                }
+                // specials (MSV_HMM.cpp:107-110), J and C as per-lane partials
+                J = fmaxf(J + loop, E + a.tr_E_J);
+                Cp = fmaxf(Cp + loop, E + a.tr_E_C);
+                N = N + loop;
+                B = N + move;
+                if (wave_any(J >= N)) B = fmaxf(N, msvk::group_max<64>(J)) + move;
+            };
+            uint64_t i = 0;
+            for (; i + 1 < L; i += 2) {
+                row(i);
+                row(i + 1);
+            }
+            if (i < L) row(i);
+            const float sc = msvk::group_max<64>(Cp) + move;
+            if (lane == 0) {
+                if (maxcode >= 20u) {
+                    a.scores[s] = __builtin_inff();
+                    atomicOr(a.errors, msvk::kErrBadResidue);
+                } else {
+                    a.scores[s] = sc;
+                }
+            }
+        }
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(a.counter, 1u);
+        item = nwaves + __builtin_amdgcn_readfirstlane(t);
+    }
+    // the last wave to finish resets the counters for the next launch on this profile
+    if (lane == 0) {
+        __threadfence();
+        if (atomicAdd(a.counter + 1, 1u) == nwaves - 1) {
+            atomicExch(a.counter, 0u);
+            atomicExch(a.counter + 1, 0u);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// MSV filter survivors (fused P-value + stream compaction): one thread per sequence, a wave ballot and
+// one atomic per wave.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void vit_select_kernel(const float* __restrict__ scores,
+                                                         const uint64_t* __restrict__ offsets, uint64_t n, float mu,
+                                                         float lambda, double threshold, double* __restrict__ pvalues,
+                                                         uint32_t* __restrict__ select, uint32_t* __restrict__ count) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    bool pass = false;
+    if (i < n) {
+        const double p = msvk::msv_pvalue_of(scores[i], offsets[i + 1] - offsets[i], mu, lambda);
+        if (pvalues) pvalues[i] = p;
+        pass = p <= threshold;
+    }
+    const uint64_t mask = __builtin_amdgcn_ballot_w64(pass);
+    if (mask == 0) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(mask >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(mask), 0u));
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(count, static_cast<uint32_t>(__popcll(mask)));
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (pass) select[base + below] = static_cast<uint32_t>(i);
+}
+
+hipError_t launch_select(const float* scores, const uint64_t* offsets, uint64_t n, float mu, float lambda,
+                         double threshold, double* pvalues, uint32_t* select, uint32_t* count, hipStream_t stream) {
+    const uint64_t blocks = (n + 255) / 256;
+    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(vit_select_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream, scores, offsets,
+                       n, mu, lambda, threshold, pvalues, select, count);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Variant table.  treg + elds: transitions in VGPRs (7 S), match scores in LDS (20 x 64 S floats); the
+// compiler holds 10 S + ~30 VGPRs, so up to S = 22 at two waves per SIMD (8 per workgroup).  Beyond,
+// transitions move to LDS and match scores are read from L2 every row.  isc variants (insert_mode 1) read
+// insert scores from L2 and keep transitions in LDS.
+// ------------------------------------------------------------------------------------------------
+#define VIT_VARIANT(S_, NT_, ELDS_, ISC_, W_, PD_, NAME_)                                                \
+    VitVariant{S_,                                                                                       \
+               NT_,                                                                                      \
+               ELDS_,                                                                                    \
+               ISC_,                                                                                     \
+               W_,                                                                                       \
+               reinterpret_cast<const void*>(&vit_kernel<S_, NT_, ELDS_, ISC_, W_, PD_>),                 \
+               NAME_,                                                                                    \
+               (ELDS_ ? kRows * (S_)*kLanes * 4 : 0) + (kTransitions - (NT_)) * (S_)*kLanes * 4}
+
+const VitVariant* vit_variants(int* count) {
+    static const VitVariant all[] = {
+        // every transition array in VGPRs, match scores in LDS
+        VIT_VARIANT(2, 7, true, false, 8, 0, "vit_s2_t7"),
+        VIT_VARIANT(4, 7, true, false, 8, 0, "vit_s4_t7"),
+        VIT_VARIANT(6, 7, true, false, 8, 0, "vit_s6_t7"),
+        VIT_VARIANT(8, 7, true, false, 8, 0, "vit_s8_t7"),
+        VIT_VARIANT(10, 7, true, false, 8, 0, "vit_s10_t7"),
+        VIT_VARIANT(12, 7, true, false, 8, 0, "vit_s12_t7"),
+        VIT_VARIANT(14, 7, true, false, 8, 0, "vit_s14_t7"),
+        VIT_VARIANT(16, 7, true, false, 8, 0, "vit_s16_t7"),
+        VIT_VARIANT(18, 7, true, false, 8, 0, "vit_s18_t7"),
+        // five arrays in VGPRs, the D chain's two (MD, DD) in LDS
+        VIT_VARIANT(16, 5, true, false, 8, 1, "vit_s16_t5"),
+        VIT_VARIANT(18, 5, true, false, 8, 1, "vit_s18_t5"),
+        VIT_VARIANT(20, 5, true, false, 8, 1, "vit_s20_t5"),
+        VIT_VARIANT(22, 5, true, false, 8, 1, "vit_s22_t5"),
+        VIT_VARIANT(24, 5, true, false, 8, 1, "vit_s24_t5"),
+        // every transition array in LDS, match scores in LDS
+        VIT_VARIANT(16, 0, true, false, 8, 1, "vit_s16_t0"),
+        VIT_VARIANT(22, 0, true, false, 8, 1, "vit_s22_t0"),
+        // transitions in LDS, match scores from L2
+        VIT_VARIANT(28, 0, false, false, 8, 3, "vit_s28_t0g"),
+        VIT_VARIANT(32, 0, false, false, 8, 3, "vit_s32_t0g"),
+        VIT_VARIANT(38, 0, false, false, 8, 3, "vit_s38_t0g"),
+        VIT_VARIANT(48, 0, false, false, 8, 3, "vit_s48_t0g"),
+        VIT_VARIANT(64, 0, false, false, 8, 3, "vit_s64_t0g"),
+        // informative insert scores (insert_mode 1): transitions in LDS, match and insert scores from L2
+        VIT_VARIANT(2, 0, false, true, 8, 3, "vit_s2_t0gi"),
+        VIT_VARIANT(8, 0, false, true, 8, 3, "vit_s8_t0gi"),
+        VIT_VARIANT(16, 0, false, true, 8, 3, "vit_s16_t0gi"),
+        VIT_VARIANT(22, 0, false, true, 8, 3, "vit_s22_t0gi"),
+        VIT_VARIANT(32, 0, false, true, 8, 3, "vit_s32_t0gi"),
+        VIT_VARIANT(38, 0, false, true, 8, 3, "vit_s38_t0gi"),
+        VIT_VARIANT(64, 0, false, true, 8, 3, "vit_s64_t0gi"),
+    };
+    *count = static_cast<int>(sizeof(all) / sizeof(all[0]));
+    return all;
+}
+
+hipError_t vit_launch(const VitVariant& v, uint32_t blocks, const VitArgs& args, hipStream_t stream, hipEvent_t start,
+                      hipEvent_t stop) {
+    void* params[] = {const_cast<VitArgs*>(&args)};
+    if (start || stop)
+        return hipExtLaunchKernel(v.fn, dim3(blocks), dim3(v.waves * 64), params, 0, stream, start, stop, 0);
+    return hipLaunchKernel(v.fn, dim3(blocks), dim3(v.waves * 64), params, 0, stream);
+}
+
+}  // namespace vitk

@@ -121,6 +121,45 @@ def homolog_batch(match_emissions: np.ndarray, seed: int, n: int, lmin: int, lma
     return codes, offsets
 
 
+def gapped_homolog_batch(match_emissions: np.ndarray, seed: int, n: int, lmin: int, lmax: int,
+                         p_delete: float = 0.03, max_delete: int = 60, p_insert: float = 0.03,
+                         max_insert: int = 8, mutate: float = 0.05) -> tuple[np.ndarray, np.ndarray]:
+    """Sequences emitted along a profile path WITH gaps: from a random start node, each step either emits
+    from the current match state, skips a run of 1..max_delete nodes (a deletion: the Viterbi path goes
+    through D states, often across the 64-lane kernel's lane boundaries), or emits 1..max_insert uniform
+    residues (an insertion: I states); uniform flanks around the core.  These are the sequences whose best
+    Viterbi path uses I and D states, which homolog_batch's ungapped cores never do."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    probs = np.asarray(match_emissions, np.float64)[1:]
+    leng = probs.shape[0]
+    cdf = np.cumsum(probs / probs.sum(axis=1, keepdims=True), axis=1)
+    seqs = []
+    for _ in range(n):
+        L = int(rng.integers(lmin, lmax + 1))
+        core_target = int(rng.integers(max(1, L // 2), L + 1))
+        k = int(rng.integers(0, max(1, leng // 3)))
+        core = []
+        while k < leng and len(core) < core_target:
+            u = rng.random()
+            if u < p_delete:
+                k += int(rng.integers(1, max_delete + 1))
+                continue
+            if u < p_delete + p_insert:
+                core.extend(rng.integers(0, 20, size=int(rng.integers(1, max_insert + 1))).tolist())
+            x = int(min((cdf[k] < rng.random()).sum(), 19))
+            core.append(int(rng.integers(0, 20)) if rng.random() < mutate else x)
+            k += 1
+        core = np.array(core[:L], np.uint8)
+        left = int(rng.integers(0, L - len(core) + 1))
+        seq = rng.integers(0, 20, size=L, dtype=np.uint8)
+        seq[left:left + len(core)] = core
+        seqs.append(seq)
+    offsets = np.zeros(n + 1, np.uint64)
+    np.cumsum([len(s) for s in seqs], out=offsets[1:])
+    codes = np.concatenate(seqs) if seqs else np.zeros(0, np.uint8)
+    return codes, offsets
+
+
 def concat_batches(*batches: tuple[np.ndarray, np.ndarray]) -> tuple[np.ndarray, np.ndarray]:
     """Concatenate CSR batches (codes, offsets) in order."""
     codes = np.concatenate([c for c, _ in batches])

@@ -298,6 +298,100 @@ msv_status msv_pvalues(const float* scores, const uint64_t* offsets, uint64_t n,
 msv_status msv_pvalues_device(int device, const float* d_scores, const uint64_t* d_offsets, uint64_t n, float mu,
                               float lambda, double* d_pvalues, void* stream);
 
+/* MSV filter on the device: the P-value of every score (the formula above, written to d_pvalues when it
+ * is not NULL) and the indices of the sequences with P <= threshold appended to d_selected (n uint32 of
+ * room; their order is arbitrary), their number in *d_count (one device uint32, zeroed here first).
+ * The survivors list feeds msv_vit_score_batch_device directly (no host round trip). */
+msv_status msv_filter_select_device(int device, const float* d_scores, const uint64_t* d_offsets, uint64_t n,
+                                    float mu, float lambda, double threshold, double* d_pvalues,
+                                    uint32_t* d_selected, uint32_t* d_count, void* stream);
+
+/* ---- Viterbi stage -----------------------------------------------------------
+ * The reference parses everything a Viterbi filter needs -- insert_emissions and the 7 transitions
+ * per node (data_readers/Profile_HMM.hpp:28-29, Profile_HMM.cpp:107-120) and STATS LOCAL VITERBI
+ * (Profile_HMM.cpp:86-87) -- and never uses it; its README (README.md:2-3) names the Viterbi algorithm
+ * as the project's point.  This stage scores HMMER3's generic local Viterbi (p7_GViterbi's recurrence,
+ * multihit local mode) over that parse, with the MSV path's own specials (MSV_HMM.cpp:49-64):
+ *   M(i,k) = max(M(i-1,k-1)+tMM, I(i-1,k-1)+tIM, D(i-1,k-1)+tDM, B(i-1)+tr_B_Mk) + match[r][k]
+ *   I(i,k) = max(M(i-1,k)+tMI, I(i-1,k)+tII) + insert[r][k]        k < LENG (no I at node LENG)
+ *   D(i,k) = max(M(i,k-1)+tMD, D(i,k-1)+tDD)
+ *   E = max_k M(i,k) (local exits; D(i,LENG) never exceeds it); J, C, N, B and the final C(L) + tr_move
+ *   exactly as MSV_HMM::run_on_sequence (MSV_HMM.cpp:100-112, per-length tr_loop / tr_move).
+ * Transition t of node k is read from transition_scores[k * 7 + t] (order m->m m->i m->d i->m i->i d->m
+ * d->d, as the .hmm file) for nodes 1 .. LENG-1 only: node 0 (B) enters through tr_B_Mk, node LENG has
+ * no successor -- so the '*' entries (which the reference parses as probability 1) are never read.
+ * There is no reference implementation ("parity unpinned"): the device scores equal the serial
+ * restatement in oracle/ bit for bit, and the stage is pinned statistically against every profile's
+ * STATS LOCAL VITERBI (tests/). */
+typedef struct msv_vit_profile msv_vit_profile;
+
+typedef enum msv_insert_mode {
+    MSV_INSERTS_ZERO = 0,    /* HMMER3's convention: insert emissions score 0 (background)          */
+    MSV_INSERTS_LOG_ODDS = 1 /* logf(insert_emissions[k][r] / background[r]) of the reference's parse */
+} msv_insert_mode;
+
+/* Score tables of the Viterbi stage from a parsed profile (model_length = M = LENG + 1):
+ * match_scores [20][M] (== msv_hmm_msv_scores' table), insert_scores [20][M] (0, or the log-odds),
+ * transition_scores [M][7] = logf(parsed probability).  Any output pointer may be NULL. */
+msv_status msv_hmm_viterbi_scores(const msv_hmm* hmm, int insert_mode, float* match_scores, float* insert_scores,
+                                  float* transition_scores, float* tr_B_Mk, float* tr_E_C, float* tr_E_J);
+
+/* The serial CPU Viterbi of one sequence (this library's own restatement, two rolling rows; the
+ * reference-shaped Viterbi_HMM::run_on_sequence in msv_hmm.hpp).  codes 0..19; a code >= 20 gives
+ * MSV_ERR_BAD_RESIDUE.  insert_scores NULL = zero insert scores. */
+msv_status msv_vit_cpu_score(const float* match_scores, const float* insert_scores, const float* transition_scores,
+                             uint32_t model_length, float tr_B_Mk, float tr_E_C, float tr_E_J, const uint8_t* codes,
+                             uint64_t L, float* score);
+
+/* Device-resident Viterbi profile.  insert_scores NULL = zero insert scores (MSV_INSERTS_ZERO). */
+msv_status msv_vit_profile_create(int device, const float* match_scores, const float* insert_scores,
+                                  const float* transition_scores, uint32_t model_length, float tr_B_Mk, float tr_E_C,
+                                  float tr_E_J, msv_vit_profile** out);
+msv_status msv_vit_profile_create_from_hmm(int device, const msv_hmm* hmm, int insert_mode, msv_vit_profile** out);
+void msv_vit_profile_destroy(msv_vit_profile* profile);
+msv_status msv_vit_profile_reserve_length(msv_vit_profile* profile, uint64_t max_length);
+
+typedef struct msv_vit_info {
+    uint32_t model_length;    /* LENG + 1                                                   */
+    uint32_t states_per_lane; /* S: one sequence per 64-lane wave, 64 * S >= LENG             */
+    uint32_t transitions_in_registers; /* of the 7 per-slot transition arrays (the rest in LDS) */
+    uint32_t match_in_lds;    /* match scores staged in LDS (else read from L2 every row)    */
+    uint32_t insert_scores;   /* informative insert scores (read from L2)                    */
+    uint32_t waves_per_block;
+    uint32_t blocks;          /* persistent grid of a full launch                           */
+    uint32_t lds_bytes;
+    uint32_t max_length;
+    int device;
+    char variant[64];
+} msv_vit_info;
+msv_status msv_vit_profile_describe(const msv_vit_profile* profile, msv_vit_info* out);
+int msv_vit_variant_count(void);
+const char* msv_vit_variant_name(int i);
+/* Force one compiled variant (tuning / tests); every variant returns identical scores. */
+msv_status msv_vit_profile_set_variant(msv_vit_profile* profile, const char* name);
+
+/* Device-resident batch, enqueued on `stream` (NULL = the library's stream).  d_select (optional): the
+ * indices of the sequences to score, *d_select_count of them when d_select_count is given (a device
+ * uint32, e.g. msv_filter_select_device's d_count), else n of them; NULL = every sequence.  Scores are
+ * written at the sequence's index in d_scores (others untouched).  An empty sequence scores -inf; errors
+ * (bad residue: +inf score, too long: NaN) are latched for msv_vit_profile_check. */
+msv_status msv_vit_score_batch_device(msv_vit_profile* profile, const uint8_t* d_residues, uint64_t residues_len,
+                                      const uint64_t* d_offsets, uint64_t n, const uint32_t* d_select,
+                                      const uint32_t* d_select_count, float* d_scores, void* stream);
+/* Host buffers in and out, synchronous (every sequence scored). */
+msv_status msv_vit_score_batch(msv_vit_profile* profile, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
+                               float* scores, void* stream);
+msv_status msv_vit_profile_check(msv_vit_profile* profile, void* stream);
+
+/* The filter pipeline on host buffers (HMMER3's MSV -> Viterbi cascade): MSV scores of every sequence
+ * (msv_score_batch_device, longest-first), P-values against (msv_mu, msv_lambda), then the Viterbi
+ * score of every sequence with P <= F1; msv_scores[n], passed[n] (0/1) and vit_scores[n] (-inf where not
+ * passed) are written, *n_passed = the survivors' count.  Everything between upload and download
+ * stays on the device.  msv and vit must live on one device. */
+msv_status msv_vit_filter_batch(msv_profile* msv, msv_vit_profile* vit, const uint8_t* residues,
+                                const uint64_t* offsets, uint64_t n, float msv_mu, float msv_lambda, double F1,
+                                float* msv_scores, uint8_t* passed, float* vit_scores, uint64_t* n_passed);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

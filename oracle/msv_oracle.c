@@ -7,6 +7,9 @@
  *   - MSV host precompute              algorithms/MSV_HMM.cpp:35-57
  *   - per-sequence transitions         algorithms/MSV_HMM.cpp:59-64
  *   - the MSV dynamic programme        algorithms/MSV_HMM.cpp:74-113
+ *   - the Viterbi stage over the parse the reference never scores with
+ *     (Profile_HMM.cpp:107-120): HMMER3's generic local Viterbi, PARITY UNPINNED (no reference
+ *     implementation exists; see the section below)
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this file's
  * shared object.  The product (hmm_fasta_viterbi_amd/, libmsv_hip.so) never links it.
@@ -253,11 +256,148 @@ void oracle_msv_run_batch(const oracle_msv* m, const uint8_t* codes, const uint6
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* Viterbi stage -- PARITY UNPINNED                                           */
+/*                                                                                            */
+/* The reference parses everything a Viterbi filter needs -- insert_emissions and the 7       */
+/* transitions per node (Profile_HMM.hpp:28-29, Profile_HMM.cpp:107-120), STATS LOCAL VITERBI */
+/* (Profile_HMM.cpp:86-87) -- and never uses it; there is no reference implementation, and    */
+/* HMMER/pyhmmer are absent here.  This is a serial restatement of HMMER3's published generic  */
+/* local Viterbi (p7_GViterbi, multihit local mode) over the reference's parse, with the MSV    */
+/* path's own specials so the two stages share one null model:                                 */
+/*   - match scores  = the MSV table, logf(p / bg) (MSV_HMM.cpp:38-45);                        */
+/*   - insert scores = 0 (HMMER3 hardwires them to the background, insert_mode 0), or          */
+/*                     logf(ins / bg) of the parsed insert_emissions (insert_mode 1);          */
+/*   - transitions   = logf(p) of the parsed probabilities (p = expf(-x), Profile_HMM.cpp:41); */
+/*                     only nodes 1 .. LENG-1 are read ('*' entries, which the reference parses */
+/*                     as p = 1, sit at node 0 and node LENG and are never read);              */
+/*   - B->Mk entry   = tr_B_Mk, E->C = tr_E_C, E->J = tr_E_J, N/C/J loop and move = the        */
+/*                     per-length tr_loop / tr_move (MSV_HMM.cpp:49-64);                       */
+/*   - exits         = E from every M_k (local) and from D_LENG; I_LENG does not exist.        */
+/* Row i, residue r (k = 1 .. LENG, M/I/D(i, 0) = -inf, row 0 all -inf but N = 0, B = move):  */
+/*   M(i,k) = max(M(i-1,k-1)+tMM(k-1), I(i-1,k-1)+tIM(k-1), D(i-1,k-1)+tDM(k-1), B(i-1)+tBM)   */
+/*            + msc[r][k]                                                                      */
+/*   I(i,k) = max(M(i-1,k)+tMI(k), I(i-1,k)+tII(k)) + isc[r][k]            (k < LENG)          */
+/*   D(i,k) = max(M(i,k-1)+tMD(k-1), D(i,k-1)+tDD(k-1))                                         */
+/*   E = max(max_k M(i,k), D(i,LENG));  J, C, N, B as MSV_HMM.cpp:107-110                      */
+/* score = C(L) + move.  Every term is one float add; max is exact, so only the adds matter.   */
+/* ------------------------------------------------------------------------------------------ */
+enum { T_MM = 0, T_MI = 1, T_MD = 2, T_IM = 3, T_II = 4, T_DM = 5, T_DD = 6 };
+
+typedef struct {
+    size_t model_length; /* LENG + 1 */
+    float* msc;          /* [20][model_length] match scores (the MSV table) */
+    float* isc;          /* [20][model_length] insert scores */
+    float* tsc;          /* [model_length][7] log transitions */
+    float tr_B_Mk, tr_E_C, tr_E_J;
+} oracle_vit;
+
+int oracle_vit_init(const oracle_hmm* h, const oracle_msv* m, int insert_mode, oracle_vit* v) {
+    const size_t M = h->model_length;
+    memset(v, 0, sizeof(*v));
+    v->model_length = M;
+    v->msc = (float*)malloc(sizeof(float) * NUM_AA * M);
+    v->isc = (float*)malloc(sizeof(float) * NUM_AA * M);
+    v->tsc = (float*)malloc(sizeof(float) * NUM_TR * M);
+    if (!v->msc || !v->isc || !v->tsc) return -1;
+    memcpy(v->msc, m->emission_scores, sizeof(float) * NUM_AA * M);
+    for (size_t k = 0; k < M; ++k)
+        for (size_t r = 0; r < NUM_AA; ++r)
+            v->isc[r * M + k] = insert_mode
+                                    ? logf(h->insert_emissions[k * NUM_AA + r] / background_frequencies[r])
+                                    : 0.0f;
+    for (size_t k = 0; k < M * NUM_TR; ++k) v->tsc[k] = logf(h->transitions[k]);
+    v->tr_B_Mk = m->tr_B_Mk;
+    v->tr_E_C = m->tr_E_C;
+    v->tr_E_J = m->tr_E_J;
+    return 0;
+}
+
+void oracle_vit_free(oracle_vit* v) {
+    free(v->msc);
+    free(v->isc);
+    free(v->tsc);
+    memset(v, 0, sizeof(*v));
+}
+
+static float fmax_ref(float a, float b) { return (a < b) ? b : a; } /* std::max(a, b) */
+
+/* Serial generic Viterbi over codes 0..19 (two rolling rows of M, I, D).  NAN for a code >= 20. */
+float oracle_vit_run_codes(const oracle_vit* v, const uint8_t* codes, size_t L) {
+    const float ninf = -INFINITY;
+    float tr_loop, tr_move;
+    oracle_seq_transitions(L, &tr_loop, &tr_move);
+    const size_t Mlen = v->model_length, K = Mlen - 1; /* K = LENG match states */
+    float* buf = (float*)malloc(sizeof(float) * 6 * Mlen);
+    if (!buf) return NAN;
+    float *pM = buf, *pI = buf + Mlen, *pD = buf + 2 * Mlen;
+    float *cM = buf + 3 * Mlen, *cI = buf + 4 * Mlen, *cD = buf + 5 * Mlen;
+    for (size_t k = 0; k < 6 * Mlen; ++k) buf[k] = ninf;
+    float N = 0.0f, B = tr_move, J = ninf, C = ninf;
+    /* t(k, x): transition x out of node k, -inf at node 0 (B enters through tr_B_Mk only) */
+#define TSC(k, x) ((k) == 0 ? ninf : v->tsc[(k) * NUM_TR + (x)])
+    for (size_t i = 1; i <= L; ++i) {
+        const unsigned r = codes[i - 1];
+        if (r >= NUM_AA) { free(buf); return NAN; }
+        const float* ms = v->msc + (size_t)r * Mlen;
+        const float* is = v->isc + (size_t)r * Mlen;
+        float E = ninf;
+        cM[0] = cI[0] = cD[0] = ninf;
+        for (size_t k = 1; k <= K; ++k) {
+            float sc = fmax_ref(pM[k - 1] + TSC(k - 1, T_MM), pI[k - 1] + TSC(k - 1, T_IM));
+            sc = fmax_ref(sc, pD[k - 1] + TSC(k - 1, T_DM));
+            sc = fmax_ref(sc, B + v->tr_B_Mk);
+            cM[k] = sc + ms[k];
+            E = fmax_ref(E, cM[k]);
+            cI[k] = (k < K) ? fmax_ref(pM[k] + TSC(k, T_MI), pI[k] + TSC(k, T_II)) + is[k] : ninf;
+            cD[k] = fmax_ref(cM[k - 1] + TSC(k - 1, T_MD), cD[k - 1] + TSC(k - 1, T_DD));
+        }
+        E = fmax_ref(E, cD[K]);
+        J = fmax_ref(J + tr_loop, E + v->tr_E_J);
+        C = fmax_ref(C + tr_loop, E + v->tr_E_C);
+        N = N + tr_loop;
+        B = fmax_ref(N + tr_move, J + tr_move);
+        float* t;
+        t = pM; pM = cM; cM = t;
+        t = pI; pI = cI; cI = t;
+        t = pD; pD = cD; cD = t;
+    }
+#undef TSC
+    free(buf);
+    return C + tr_move;
+}
+
+void oracle_vit_run_batch(const oracle_vit* v, const uint8_t* codes, const uint64_t* offsets, size_t n,
+                          float* scores) {
+    for (size_t s = 0; s < n; ++s)
+        scores[s] = oracle_vit_run_codes(v, codes + offsets[s], (size_t)(offsets[s + 1] - offsets[s]));
+}
+
+/* The same DP over caller tables (msc, isc [20][M], tsc [M][7] log transitions; isc NULL = zero): for
+ * synthetic models (e.g. transitions that reduce Viterbi to MSV, or near-free D->D chains). */
+void oracle_vit_score_tables(const float* msc, const float* isc, const float* tsc, size_t model_length,
+                             float tr_B_Mk, float tr_E_C, float tr_E_J, const uint8_t* codes,
+                             const uint64_t* offsets, size_t n, float* scores) {
+    oracle_vit v;
+    v.model_length = model_length;
+    v.msc = (float*)msc;
+    v.tsc = (float*)tsc;
+    v.isc = (float*)calloc(NUM_AA * model_length, sizeof(float));
+    if (isc) memcpy(v.isc, isc, sizeof(float) * NUM_AA * model_length);
+    v.tr_B_Mk = tr_B_Mk;
+    v.tr_E_C = tr_E_C;
+    v.tr_E_J = tr_E_J;
+    oracle_vit_run_batch(&v, codes, offsets, n, scores);
+    free(v.isc);
+}
+
+/* ------------------------------------------------------------------------------------------ */
 /* Convenience handle API for ctypes                                                          */
 /* ------------------------------------------------------------------------------------------ */
 typedef struct {
     oracle_hmm hmm;
     oracle_msv msv;
+    oracle_vit vit[2]; /* insert_mode 0 / 1, built on first use */
+    int vit_ready[2];
 } oracle_profile;
 
 oracle_profile* oracle_profile_load(const char* path) {
@@ -273,6 +413,8 @@ oracle_profile* oracle_profile_load(const char* path) {
 
 void oracle_profile_free(oracle_profile* p) {
     if (!p) return;
+    for (int m = 0; m < 2; ++m)
+        if (p->vit_ready[m]) oracle_vit_free(&p->vit[m]);
     oracle_msv_free(&p->msv);
     oracle_hmm_free(&p->hmm);
     free(p);
@@ -309,4 +451,25 @@ float oracle_profile_score_string(const oracle_profile* p, const char* seq) {
 void oracle_profile_score_batch(const oracle_profile* p, const uint8_t* codes, const uint64_t* offsets,
                                 size_t n, float* scores) {
     oracle_msv_run_batch(&p->msv, codes, offsets, n, scores);
+}
+
+/* Viterbi tables of insert_mode (0 = HMMER3 zero insert scores, 1 = log-odds); not thread-safe on the
+ * first call for a mode (call once before scoring from several threads). */
+static const oracle_vit* profile_vit(oracle_profile* p, int insert_mode) {
+    const int m = insert_mode ? 1 : 0;
+    if (!p->vit_ready[m]) {
+        if (oracle_vit_init(&p->hmm, &p->msv, m, &p->vit[m]) != 0) return NULL;
+        p->vit_ready[m] = 1;
+    }
+    return &p->vit[m];
+}
+int oracle_profile_vit_prepare(oracle_profile* p, int insert_mode) { return profile_vit(p, insert_mode) ? 0 : -1; }
+void oracle_profile_vit_tables(oracle_profile* p, int insert_mode, float* isc, float* tsc) {
+    const oracle_vit* v = profile_vit(p, insert_mode);
+    memcpy(isc, v->isc, sizeof(float) * NUM_AA * v->model_length);
+    memcpy(tsc, v->tsc, sizeof(float) * NUM_TR * v->model_length);
+}
+void oracle_profile_vit_score_batch(oracle_profile* p, int insert_mode, const uint8_t* codes,
+                                    const uint64_t* offsets, size_t n, float* scores) {
+    oracle_vit_run_batch(profile_vit(p, insert_mode), codes, offsets, n, scores);
 }

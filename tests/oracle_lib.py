@@ -52,6 +52,12 @@ def oracle():
         L.oracle_profile_score_string.argtypes = [vp, C.c_char_p]
         L.oracle_profile_score_batch.argtypes = [vp, vp, vp, C.c_size_t, vp]
         L.oracle_seq_transitions.argtypes = [C.c_size_t, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.oracle_profile_vit_prepare.restype = C.c_int
+        L.oracle_profile_vit_prepare.argtypes = [vp, C.c_int]
+        L.oracle_profile_vit_tables.argtypes = [vp, C.c_int, vp, vp]
+        L.oracle_profile_vit_score_batch.argtypes = [vp, C.c_int, vp, vp, C.c_size_t, vp]
+        L.oracle_vit_score_tables.argtypes = [vp, vp, vp, C.c_size_t, C.c_float, C.c_float, C.c_float, vp, vp,
+                                              C.c_size_t, vp]
         _oracle = L
     return _oracle
 
@@ -107,6 +113,39 @@ class OracleProfile:
             list(ex.map(lambda k: run(int(cuts[k]), int(cuts[k + 1])), range(threads)))
         return out
 
+    def vit_tables(self, insert_mode: int = 0):
+        """(insert scores [20][M], log transitions [M][7]) of the Viterbi restatement."""
+        M = self.model_length
+        isc = np.zeros((20, M), np.float32)
+        tsc = np.zeros((M, 7), np.float32)
+        assert self.L.oracle_profile_vit_prepare(self.p, insert_mode) == 0
+        self.L.oracle_profile_vit_tables(self.p, insert_mode, isc.ctypes.data, tsc.ctypes.data)
+        return isc, tsc
+
+    def vit_score_batch(self, codes: np.ndarray, offsets: np.ndarray, insert_mode: int = 0,
+                        threads: int = 1) -> np.ndarray:
+        """Viterbi-stage scores of the serial restatement (oracle_vit_run_codes)."""
+        codes = np.ascontiguousarray(codes, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        n = len(offsets) - 1
+        out = np.zeros(n, np.float32)
+        assert self.L.oracle_profile_vit_prepare(self.p, insert_mode) == 0
+        base = codes.ctypes.data if codes.size else None
+
+        def run(lo, hi):
+            if hi > lo:
+                self.L.oracle_profile_vit_score_batch(self.p, insert_mode, base, offsets[lo:].ctypes.data, hi - lo,
+                                                      out[lo:].ctypes.data)
+
+        if threads <= 1 or n < 2 * threads:
+            run(0, n)
+            return out
+        from concurrent.futures import ThreadPoolExecutor
+        cuts = np.linspace(0, n, threads + 1).astype(np.int64)
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(lambda k: run(int(cuts[k]), int(cuts[k + 1])), range(threads)))
+        return out
+
     def score_string(self, seq: str) -> float:
         return float(self.L.oracle_profile_score_string(self.p, seq.encode()))
 
@@ -114,6 +153,22 @@ class OracleProfile:
         if getattr(self, "p", None):
             self.L.oracle_profile_free(self.p)
             self.p = None
+
+
+def vit_score_tables(msc, isc, tsc, consts, codes, offsets) -> np.ndarray:
+    """The oracle's Viterbi DP over caller tables (msc/isc [20][M], tsc [M][7]; isc None = zero)."""
+    L = oracle()
+    msc = np.ascontiguousarray(msc, np.float32)
+    tsc = np.ascontiguousarray(tsc, np.float32)
+    isc = None if isc is None else np.ascontiguousarray(isc, np.float32)
+    codes = np.ascontiguousarray(codes, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = len(offsets) - 1
+    out = np.zeros(n, np.float32)
+    L.oracle_vit_score_tables(msc.ctypes.data, None if isc is None else isc.ctypes.data, tsc.ctypes.data,
+                              msc.shape[1], *[float(x) for x in consts], codes.ctypes.data if codes.size else None,
+                              offsets.ctypes.data, n, out.ctypes.data)
+    return out
 
 
 def make_batch(seed: int, lengths) -> tuple[np.ndarray, np.ndarray]:
