@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may run on")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-viterbi", action="store_true", help="skip the informational Viterbi-stage figure")
+    ap.add_argument("--no-clock", action="store_true", help="time the steps without the in-kernel clock stamps")
     ap.add_argument("--no-order", action="store_true", help="dequeue in input order (no longest-first sort)")
     ap.add_argument("--no-launch-events", action="store_true",
                     help="diagnostic: time the steps without the MSV launch's start/stop events (kernel_ms null)")
@@ -177,6 +179,125 @@ def cpu_baseline(profile_path, codes, offsets, gpu_scores, target_s, threads):
         "bitwise_equal_to_gpu": match,
         "single_thread": single,
         "cpu_model": cpu_model(),
+    }
+
+
+VIT_OPS_PER_CELL = 14  # fp32 ops per Viterbi DP cell (msv.h): M 3 adds + 3 max + 1 add, I 2 + 1, D 2 + 1, E 1
+
+
+def viterbi_stage(args, msv_engine, prof_path, dev, stream, d_res, residues, d_off, n, d_scores, codes, offsets,
+                  lmax, leng, hip_event, hip_elapsed_ms, F1=0.02):
+    """Information, never `value`: the Viterbi stage on this batch's MSV survivors.  The
+    timed steps' device scores -> msv_filter_select_device (P <= F1 against STATS LOCAL MSV, on the GPU)
+    -> ONE Viterbi launch over the survivors list (count read on the device), timed with HIP events the
+    launch itself updates.  Roofline: 14 fp32 add/max ops per cell (cells = survivor residues x LENG).
+    CPU baseline: the oracle's serial Viterbi ("port") on a bounded sample of the survivors, on the host
+    threads, whose scores are also compared bitwise with the kernel's."""
+    import torch
+
+    import hmm_fasta_viterbi_amd as msv
+    from hmm_fasta_viterbi_amd import _native
+    native = _native.lib()
+    native.msv_vit_debug_time_next_launch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    h = msv.Profile_HMM(prof_path)
+    vit = msv.Viterbi_HMM(h, device=dev.index or 0)
+    vit.reserve_length(lmax)
+    sh = stream.cuda_stream
+    d_sel = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    d_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    d_vsc = torch.full((max(n, 1),), float("-inf"), dtype=torch.float32, device=dev)
+    from hmm_fasta_viterbi_amd._native import check
+    check(native.msv_filter_select_device(dev.index or 0, d_scores.data_ptr(), d_off.data_ptr(), n, msv_engine.msv_mu,
+                                          msv_engine.msv_lambda, F1, None, d_sel.data_ptr(), d_cnt.data_ptr(), sh))
+
+    def launch(ev=None):
+        if ev is not None:
+            native.msv_vit_debug_time_next_launch(vit._p, ev[0], ev[1])
+        vit.score_batch_device(d_res.data_ptr(), residues, d_off.data_ptr(), n, d_vsc.data_ptr(), d_sel.data_ptr(),
+                               d_cnt.data_ptr(), sh)
+
+    for _ in range(3):
+        launch()
+    torch.cuda.synchronize(dev)
+    steps = max(3, args.steps // 2)
+    events = [(hip_event(), hip_event()) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for ev in events:
+        launch(ev)
+    torch.cuda.synchronize(dev)
+    wall_ms = (time.perf_counter() - t0) / steps * 1e3
+    vit.check(sh)
+    kms = float(np.mean([hip_elapsed_ms(a, b) for a, b in events]))
+    cnt = int(d_cnt.item())
+    sel = np.sort(d_sel[:cnt].cpu().numpy().view(np.uint32))
+    vsc = d_vsc[:n].cpu().numpy()
+    lens = np.diff(offsets.astype(np.int64))
+    surv_res = int(lens[sel].sum())
+    cells = surv_res * leng
+    achieved = VIT_OPS_PER_CELL * cells / (kms * 1e-3) / 1e12
+    info = vit.describe()
+    # CPU port baseline on a bounded sample of the survivors (the oracle's serial DP, one profile per run)
+    ora = C.CDLL(os.path.join(ROOT, "oracle", "_build", "libmsv_oracle.so"))
+    ora.oracle_profile_load.restype = C.c_void_p
+    ora.oracle_profile_load.argtypes = [C.c_char_p]
+    ora.oracle_profile_vit_prepare.argtypes = [C.c_void_p, C.c_int]
+    ora.oracle_profile_vit_score_batch.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t,
+                                                   C.c_void_p]
+    ora.oracle_profile_free.argtypes = [C.c_void_p]
+    op = ora.oracle_profile_load(prof_path.encode())
+    ora.oracle_profile_vit_prepare(op, 0)
+    threads = cpu_threads(args.cpu_threads)
+    sub_off = np.zeros(len(sel) + 1, np.uint64)
+    np.cumsum(lens[sel], out=sub_off[1:])
+    sub_codes = np.concatenate([codes[int(offsets[s]):int(offsets[s + 1])] for s in sel]) if cnt else codes[:0]
+    sub_codes = np.ascontiguousarray(sub_codes)
+
+    def cpu_run(m):
+        out = np.zeros(m, np.float32)
+        cuts = np.linspace(0, m, threads + 1).astype(np.int64)
+        from concurrent.futures import ThreadPoolExecutor
+
+        def part(k):
+            lo, hi = int(cuts[k]), int(cuts[k + 1])
+            if hi > lo:
+                ora.oracle_profile_vit_score_batch(op, 0, sub_codes.ctypes.data, sub_off[lo:].ctypes.data, hi - lo,
+                                                   out[lo:].ctypes.data)
+        t = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(part, range(threads)))
+        return time.perf_counter() - t, out
+
+    cpu = None
+    if cnt and not args.no_cpu:
+        m0 = min(cnt, 2 * threads)
+        sec, _ = cpu_run(m0)
+        m = int(min(cnt, max(m0, args.cpu_seconds / 3 / max(sec, 1e-6) * m0)))
+        sec, out = cpu_run(m)
+        res_m = int(sub_off[m])
+        cpu = {"value": round(res_m / sec / 1e6, 4), "unit": "M residues/s", "cores": threads, "kind": "port",
+               "sample": f"first {m} of {cnt} survivors ({res_m} residues), {sec:.2f} s on {threads} host threads "
+                         "(oracle_vit_run_codes, serial restatement)",
+               "bitwise_equal_to_gpu": bool(np.array_equal(out.view(np.uint32), vsc[sel[:m]].view(np.uint32)))}
+    ora.oracle_profile_free(op)
+    return {
+        "F1": F1,
+        "survivors": cnt,
+        "survivor_fraction": round(cnt / max(n, 1), 5),
+        "survivor_residues": surv_res,
+        "kernel_variant": info["variant"],
+        "kernel_ms": round(kms, 4),
+        "ms_per_launch_wall": round(wall_ms, 4),
+        "M_residues_s": round(surv_res / (kms * 1e-3) / 1e6, 2),
+        "gcups": round(cells / (kms * 1e-3) / 1e9, 2),
+        "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 2),
+                     "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
+                     "note": f"{VIT_OPS_PER_CELL} fp32 add/max ops per Viterbi cell (M: 3 transition adds, 3 max, "
+                             "1 emission add; I: 2 adds, 1 max; D: 2 adds, 1 max; E: 1 max), cells = survivor "
+                             "residues x LENG; kernel time from the launch's own HIP events"},
+        "scores_finite": bool(np.all(np.isfinite(vsc[sel]))),
+        "cpu_baseline": cpu,
+        "note": "information, not `value`: the MSV filter's survivors (P <= F1, STATS LOCAL MSV) of the timed "
+                "batch, selected on the device, scored by the Viterbi stage in one launch",
     }
 
 
@@ -342,13 +463,18 @@ def main(args=None):
         assert hip.hipEventElapsedTime(C.byref(ms), a, b) == 0
         return float(ms.value)
 
-    def step(ev=None):
+    native.msv_debug_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
+    native.msv_debug_grid_waves.argtypes = [C.c_void_p]
+
+    def step(ev=None, stamps=None):
         order_ptr = None
         if not args.no_order:
             engine.order_longest_first(d_off.data_ptr(), n, d_order.data_ptr(), sh)
             order_ptr = d_order.data_ptr()
         if ev is not None:  # the MSV launch itself updates these two HIP events (hipExtLaunchKernel)
             native.msv_debug_time_next_launch(engine._p, ev[0], ev[1])
+        if stamps is not None:  # ... and writes every wave's realtime / shader-clock stamps here
+            native.msv_debug_set_stamps(engine._p, stamps.data_ptr())
         engine.score_batch_device(d_res.data_ptr(), residues, d_off.data_ptr(), n, d_scores.data_ptr(), order_ptr, sh)
         if gathered is not None and world > 1:  # cfg4: the RCCL gather of the scores is part of the step
             with torch.cuda.stream(stream):
@@ -441,30 +567,68 @@ def main(args=None):
     # the launch stream), not event records around it -- each record is a marker packet (~4 us in the
     # stream), which would add ~8 us to every step (7% of cfg2's).
     events = [(hip_event(), hip_event()) for _ in range(args.steps)]
+    # Clock during the timed steps: every wave of each timed launch stamps its start and end in realtime
+    # (100 MHz) and shader-clock ticks (s_memtime); clock = sum of ticks / sum of realtime over the waves
+    # (the kernel's existing diagnostic branch, taken once per wave at start and end).
+    nwaves = int(native.msv_debug_grid_waves(engine._p))
+    stamp_bufs = None if args.no_clock else [torch.zeros(nwaves * 6, dtype=torch.int64, device=dev)
+                                              for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(None if args.no_launch_events else events[k])
+        step(None if args.no_launch_events else events[k], None if stamp_bufs is None else stamp_bufs[k])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    native.msv_debug_set_stamps(engine._p, None)
     engine.check(sh)
+    clock = None
+    if stamp_bufs is not None:
+        per_launch = []
+        for b in stamp_bufs:
+            a = b.cpu().numpy().reshape(nwaves, 6)
+            a = a[a[:, 1] > 0]
+            rt, ck = (a[:, 1] - a[:, 0]).sum(), (a[:, 5] - a[:, 4]).sum()
+            if rt > 0:
+                per_launch.append(float(ck) / float(rt) * 0.1)  # GHz
+        if per_launch:
+            clock = {"median": round(float(np.median(per_launch)), 4), "min": round(float(min(per_launch)), 4),
+                     "max": round(float(max(per_launch)), 4), "launches": len(per_launch)}
     elapsed = t1 - t0
     kernel_ms = float("nan") if args.no_launch_events else float(np.mean([hip_elapsed_ms(a, b) for a, b in events]))
     for a, b in events:
         hip.hipEventDestroy(a)
         hip.hipEventDestroy(b)
     residues_all = residues
+    per_rank = None
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
-        r = torch.tensor([residues], dtype=torch.int64, device=cdev)
-        dist.all_reduce(r, op=dist.ReduceOp.SUM)
-        residues_all = int(r[0])
+        # every rank's own figures (so an N-rank line explains itself: imbalance vs gather vs launch skew),
+        # then the contract's max-over-ranks time and the job's total residues
+        mine = torch.tensor([elapsed, kernel_ms, float(residues), float(n)], dtype=torch.float64, device=cdev)
+        allr = torch.empty(world * 4, dtype=torch.float64, device=cdev)
+        dist.all_gather_into_tensor(allr, mine)
+        allr = allr.cpu().numpy().reshape(world, 4)
+        elapsed, kernel_ms = float(allr[:, 0].max()), float(allr[:, 1].max())
+        residues_all = int(allr[:, 2].sum())
+
+        def spread(x):
+            x = np.asarray(x, np.float64)
+            return {"min": round(float(x.min()), 4), "max": round(float(x.max()), 4),
+                    "max_over_min": round(float(x.max() / x.min()), 4) if x.min() > 0 else None}
+        per_rank = {
+            "ms_per_step": [round(float(v) / args.steps * 1e3, 4) for v in allr[:, 0]],
+            "kernel_ms": [round(float(v), 4) for v in allr[:, 1]],
+            "residues": [int(v) for v in allr[:, 2]],
+            "sequences": [int(v) for v in allr[:, 3]],
+            "imbalance": {"ms_per_step": spread(allr[:, 0] / args.steps * 1e3), "kernel_ms": spread(allr[:, 1]),
+                          "residues": spread(allr[:, 2])},
+            "note": "each rank's own timed window (barrier-bracketed); `ms_per_step` and `kernel_ms` above are "
+                    "the max over ranks; a step's time beyond its kernel is the order launch"
+                    + (" and the in-step RCCL all-gather" if scaling == "strong" else ""),
+        }
 
     # weak configs: output collection after timing (RCCL all-gather of every rank's scores)
     gather_ms = None
@@ -534,6 +698,14 @@ def main(args=None):
                 "peak": round(VALU_PEAK_TOPS, 2),
                 "unit": "TFLOP/s",
                 "frac": round(achieved / VALU_PEAK_TOPS, 4),
+                "clock_GHz": None if clock is None else clock["median"],
+                "frac_at_clock": None if clock is None else round(
+                    achieved / (256 * 128 * clock["median"] * 1e9 / 1e12), 4),
+                "clock": None if clock is None else {
+                    **clock, "source": "in-kernel: each timed launch's waves stamp s_memtime (one tick per shader "
+                                       "cycle) and s_memrealtime (100 MHz) at start and end; clock = sum of ticks / "
+                                       "sum of realtime over the waves, median over the timed launches; "
+                                       "frac_at_clock = achieved / (256 CU x 128 lanes x clock)"},
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "note": "fp32 add/max ops: 3 per DP cell (cells = residues x LENG); peak = 256 CU x 128 "
@@ -554,6 +726,7 @@ def main(args=None):
                 "peak_GBps": HBM_PEAK_GBPS,
             },
             "gather_ms": gather_ms,
+            "per_rank": per_rank,
             "end_to_end": {
                 "host_pinned_M_residues_s": round(host_pinned, 1),
                 "host_pageable_M_residues_s": round(host_pageable, 1),
@@ -576,6 +749,9 @@ def main(args=None):
             },
             "scores_finite_and_consistent": ok,
         }
+        if not args.no_viterbi:
+            result["viterbi_stage"] = viterbi_stage(args, engine, prof_path, dev, stream, d_res, residues, d_off, n,
+                                                    d_scores, codes, offsets, lmax, leng, hip_event, hip_elapsed_ms)
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(prof_path, codes, offsets, scores, args.cpu_seconds,
                                                   cpu_threads(args.cpu_threads))

@@ -30,11 +30,14 @@ constexpr uint32_t kOrderBins = 4096;  // lengths >= 4095 share the longest bin
 // left} (and, for the longest-first order, the next histogram), so launches on different streams
 // never share a counter; a slot is reused only after its previous launch (an event wait when the
 // streams differ).  d_words: [2k, 2k+1] = slot k's counters, [kErrWord] = sticky error bits,
-// [kErrWord + 1 + a] = the error bits of asynchronous staging slot a (msv_score_batch_async).
+// [kErrWord + 1 + a] = the error bits of asynchronous staging slot a (msv_score_batch_async),
+// [kHostErrWord] = the error bits of synchronous host calls (msv_score_batch), which report and clear only
+// their own: bits latched by msv_score_batch_device launches stay for msv_profile_check.
 constexpr int kLaunchSlots = 8;
 constexpr int kAsyncSlots = 3;
 constexpr int kErrWord = 2 * kLaunchSlots;
-constexpr int kWords = kErrWord + 1 + kAsyncSlots + 1;
+constexpr int kHostErrWord = kErrWord + 1 + kAsyncSlots;
+constexpr int kWords = kHostErrWord + 1;
 // Every launch addresses < 2^32 residue bytes.
 constexpr uint64_t kChunkBytes = (1ull << 32) - (1ull << 20);
 // Host batches of at least this many residues are scored as a copy/compute pipeline of pieces.
@@ -840,9 +843,10 @@ msv_status msv_profile_set_variant(msv_profile* p, const char* name) {
     return MSV_ERR_INVALID_ARGUMENT;
 }
 
-// Diagnostics, deliberately not in msv.h: a device buffer of 4 uint64 per wave of the persistent
-// grid that receives {start, end (s_memrealtime, 100 MHz), rows issued, xcc<<32|block} for every
-// wave of subsequent launches (tools/wave_timeline.py).  nullptr switches it off.
+// Diagnostics, deliberately not in msv.h: a device buffer of msvk::kStampWords (6) uint64 per wave of the
+// persistent grid that receives {start, end (s_memrealtime, 100 MHz), rows issued, xcc<<32|block, shader
+// clock start, end (s_memtime)} for every wave of subsequent launches (tools/wave_timeline.py, bench.py's
+// clock_GHz).  nullptr switches it off.
 msv_status msv_debug_set_stamps(msv_profile* p, uint64_t* d_stamps) {
     if (!p) return MSV_ERR_INVALID_ARGUMENT;
     p->d_stamps = d_stamps;
@@ -1061,17 +1065,21 @@ msv_status msv_profile_bind_stream(msv_profile* p, void* stream) {
     return MSV_OK;
 }
 
+// Synchronises `st`, then reads, clears and reports error word `word` of the profile.
+static msv_status check_word(msv_profile* p, hipStream_t st, int word) {
+    uint32_t err = 0;
+    MSV_HIP(hipMemcpyAsync(&err, p->d_words + word, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    MSV_HIP(hipStreamSynchronize(st));
+    if (err) MSV_HIP(hipMemsetAsync(p->d_words + word, 0, sizeof(uint32_t), st));
+    MSV_HIP(hipStreamSynchronize(st));
+    return err_status(err);
+}
+
 msv_status msv_profile_check(msv_profile* p, void* stream) {
     if (!p) return MSV_ERR_INVALID_ARGUMENT;
     DeviceGuard g(p->device);
     if (!g.ok) return MSV_ERR_NO_DEVICE;
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : p->stream;
-    uint32_t err = 0;
-    MSV_HIP(hipMemcpyAsync(&err, p->d_words + kErrWord, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    MSV_HIP(hipStreamSynchronize(st));
-    if (err) MSV_HIP(hipMemsetAsync(p->d_words + kErrWord, 0, sizeof(uint32_t), st));
-    MSV_HIP(hipStreamSynchronize(st));
-    return err_status(err);
+    return check_word(p, stream ? static_cast<hipStream_t>(stream) : p->stream, kErrWord);
 }
 
 msv_status msv_order_longest_first(msv_profile* p, const uint64_t* d_offsets, uint64_t n, uint32_t* d_order,
@@ -1256,8 +1264,8 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         if (pipe) MSV_HIP(hipStreamWaitEvent(c, p->events[2 + k], 0));
         const uint8_t* src = zres ? zres + base0 + lo : (small ? d_small_res : p->d_res) + lo;
         s = launch_batch(p, bytes ? src : p->d_dummy, std::max<uint64_t>(bytes, 1), p->d_off + cut[k] + k,
-                         cut[k + 1] - cut[k], sort ? p->d_order + cut[k] : nullptr, dsc + cut[k], c, !pipe, nullptr,
-                         zres && bytes);
+                         cut[k + 1] - cut[k], sort ? p->d_order + cut[k] : nullptr, dsc + cut[k], c, !pipe,
+                         p->d_words + kHostErrWord, zres && bytes);
         if (s != MSV_OK) return s;
     }
     if (pipe) {  // join the second compute stream (done before the last piece) back into the caller's
@@ -1271,15 +1279,15 @@ msv_status msv_score_batch(msv_profile* p, const uint8_t* residues, const uint64
         drain.armed = false;
         if (staged_scores) std::memcpy(scores, p->h_sc, n * sizeof(float));
         if (scan_scores(scores, n) == MSV_OK) return MSV_OK;
-        const msv_status e = msv_profile_check(p, st);  // reads, clears and reports the latched error bits
+        const msv_status e = check_word(p, st, kHostErrWord);  // reads, clears and reports this call's bits
         return e != MSV_OK ? e : scan_scores(scores, n);
     }
     MSV_HIP(hipMemcpyAsync(scores, p->d_scores, n * sizeof(float), hipMemcpyDeviceToHost, st));
-    MSV_HIP(hipMemcpyAsync(h_err, p->d_words + kErrWord, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    MSV_HIP(hipMemcpyAsync(h_err, p->d_words + kHostErrWord, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     MSV_HIP(hipStreamSynchronize(st));  // also: the pinned h_off is rewritten by the next call
     drain.armed = false;
     if (*h_err == 0) return MSV_OK;
-    return msv_profile_check(p, st);  // reads, clears and reports the latched error bits
+    return check_word(p, st, kHostErrWord);  // reads, clears and reports this call's error bits
 }
 
 msv_status msv_score_batch_async(msv_profile* p, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
@@ -1437,15 +1445,24 @@ static msv_status coop_plan_in_layout(msv_profile* p, const msvk::CoopVariant* c
 
 // The cooperative variant a grid of n sequences x these profiles runs fused (grid_coop_fused), or nullptr:
 // a grid of few sequences (n x profiles <= kFusedMaxSeqs), every profile with tr_E_C == tr_E_J and no
-// forced variant, a variant covering the largest model.
-static const msvk::CoopVariant* fused_coop_variant(msv_profile* const* profiles, uint32_t n_profiles, uint64_t n) {
-    if (n_profiles < 2 || n * n_profiles > kFusedMaxSeqs) return nullptr;
+// forced variant, a variant covering the largest model -- and at most as many workgroups per launch (n x
+// the launch's profiles) as the smallest coop_max_n of the listed profiles: the limit of the per-profile
+// cooperative plan (about one workgroup fits a CU, so a launch of more is several rounds of the grid, and
+// past ~2 rounds the cooperative plan loses).  coop_max_n = 0 (no cooperative plan, or
+// msv_debug_set_coop_max_n(0)) turns the fused form off.  Residues read in place over PCIe
+// (host_residues) keep the latency layout, as select_plan does.
+static const msvk::CoopVariant* fused_coop_variant(msv_profile* const* profiles, uint32_t n_profiles, uint64_t n,
+                                                   bool host_residues = false) {
+    if (host_residues || n_profiles < 2 || n * n_profiles > kFusedMaxSeqs) return nullptr;
     uint32_t states = 0;
+    uint64_t cap = ~0ull;
     for (uint32_t i = 0; i < n_profiles; ++i) {
         const msv_profile* p = profiles[i];
         if (p->force || std::memcmp(&p->tr_E_C, &p->tr_E_J, sizeof(float)) != 0) return nullptr;
         states = std::max(states, p->model_length - 1);
+        cap = std::min(cap, p->coop_max_n);
     }
+    if (static_cast<uint64_t>(std::min<uint32_t>(n_profiles, msvk::kGridMaxProfiles)) * n > cap) return nullptr;
     const msvk::CoopVariant* cv = pick_coop_variant(states);
     return cv && cv->grid_fn ? cv : nullptr;
 }
@@ -1536,9 +1553,11 @@ static msv_status grid_fused(msv_profile* const* profiles, uint32_t n_profiles, 
     return MSV_OK;
 }
 
-msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* d_residues,
-                                 uint64_t residues_len, const uint64_t* d_offsets, uint64_t n,
-                                 const uint32_t* d_order, float* d_scores, void* stream) {
+// host_residues: d_residues is the device alias of page-locked host memory (msv_score_grid's in-place
+// read): no cooperative plan (fused or per profile) and the per-profile launches take the zero-copy twins.
+static msv_status score_grid_device(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* d_residues,
+                                    uint64_t residues_len, const uint64_t* d_offsets, uint64_t n,
+                                    const uint32_t* d_order, float* d_scores, void* stream, bool host_residues) {
     if (!profiles || n_profiles == 0) return MSV_ERR_INVALID_ARGUMENT;
     for (uint32_t i = 0; i < n_profiles; ++i)
         if (!profiles[i] || profiles[i]->device != profiles[0]->device) return MSV_ERR_INVALID_ARGUMENT;
@@ -1558,7 +1577,7 @@ msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profil
             for (uint32_t j = 0; j < n_profiles; ++j) same += profiles[j] == profiles[i];
             most = std::max(most, same);
         }
-        const msvk::CoopVariant* cv = fused_coop_variant(profiles, n_profiles, n);
+        const msvk::CoopVariant* cv = fused_coop_variant(profiles, n_profiles, n, host_residues);
         if (cv)
             return grid_coop_fused(profiles, n_profiles, cv, d_residues, residues_len, d_offsets, n, d_order, d_scores, cs);
         // A fused launch holds one counter slot per entry until it ends: a handle listed more often than
@@ -1587,8 +1606,8 @@ msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profil
         if (!p->done) MSV_HIP(hipEventCreateWithFlags(&p->done, hipEventDisableTiming));
         hipStream_t ps = p->stream == cs ? cs : p->stream;
         if (ps != cs) MSV_HIP(hipStreamWaitEvent(ps, fork, 0));
-        const msv_status s = msv_score_batch_device(p, d_residues, residues_len, d_offsets, n, d_order,
-                                                    d_scores + static_cast<uint64_t>(i) * n, ps);
+        const msv_status s = launch_batch(p, d_residues, residues_len, d_offsets, n, d_order,
+                                          d_scores + static_cast<uint64_t>(i) * n, ps, true, nullptr, host_residues);
         if (s != MSV_OK) return s;
         if (ps != cs) {
             MSV_HIP(hipEventRecord(p->done, ps));
@@ -1596,6 +1615,13 @@ msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profil
         }
     }
     return MSV_OK;
+}
+
+msv_status msv_score_grid_device(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* d_residues,
+                                 uint64_t residues_len, const uint64_t* d_offsets, uint64_t n,
+                                 const uint32_t* d_order, float* d_scores, void* stream) {
+    return score_grid_device(profiles, n_profiles, d_residues, residues_len, d_offsets, n, d_order, d_scores, stream,
+                             false);
 }
 
 msv_status msv_score_grid(msv_profile* const* profiles, uint32_t n_profiles, const uint8_t* residues,
@@ -1659,13 +1685,14 @@ msv_status msv_score_grid(msv_profile* const* profiles, uint32_t n_profiles, con
     const uint8_t* d_res = zres ? zres : p0->d_res;
     if (bytes && !zres) MSV_HIP(hipMemcpyAsync(p0->d_res, residues + offsets[0], bytes, hipMemcpyHostToDevice, st));
     MSV_HIP(hipMemcpyAsync(p0->d_off, p0->h_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    // (a fused cooperative grid runs one workgroup per sequence: no dequeue order to sort)
-    const bool sort = !zres ? fused_coop_variant(profiles, n_profiles, n) == nullptr : true;
+    // (a fused cooperative grid runs one workgroup per sequence: no dequeue order to sort; residues read
+    // in place never take it)
+    const bool sort = fused_coop_variant(profiles, n_profiles, n, zres != nullptr) == nullptr;
     msv_status s = sort ? msv_order_longest_first(p0, p0->d_off, n, p0->d_order, st) : MSV_OK;
     if (s != MSV_OK) return s;
     float* const dsc = direct ? direct : p0->d_scores;
-    s = msv_score_grid_device(profiles, n_profiles, bytes ? d_res : p0->d_dummy, std::max<uint64_t>(bytes, 1),
-                              p0->d_off, n, sort ? p0->d_order : nullptr, dsc, st);
+    s = score_grid_device(profiles, n_profiles, bytes ? d_res : p0->d_dummy, std::max<uint64_t>(bytes, 1), p0->d_off,
+                          n, sort ? p0->d_order : nullptr, dsc, st, zres != nullptr);
     if (s != MSV_OK) return s;
     if (!direct) MSV_HIP(hipMemcpyAsync(scores, p0->d_scores, total * sizeof(float), hipMemcpyDeviceToHost, st));
     drain.armed = false;

@@ -164,3 +164,108 @@ std::vector<Log_score> MSV_HMM::Multi_device::score_batch(const Packed_sequences
     check(s, "msv_multi_score_batch");
     return out;
 }
+
+// ---- Viterbi stage --------------------------------------------------------------------
+Viterbi_HMM::Viterbi_HMM(const Profile_HMM& base_hmm, int device, msv_insert_mode inserts)
+    : viterbi_mu(base_hmm.stats_local_viterbi_mu),
+      viterbi_lambda(base_hmm.stats_local_viterbi_lambda),
+      model_length_(base_hmm.model_length),
+      inserts_(inserts == MSV_INSERTS_LOG_ODDS) {
+    const size_t M = model_length_;
+    match_scores_.assign(NUM_OF_AMINO_ACIDS * M, 0.f);
+    insert_scores_.assign(NUM_OF_AMINO_ACIDS * M, 0.f);
+    transition_scores_.assign(NUM_OF_TRANSITIONS * M, 0.f);
+    for (size_t k = 0; k < M; ++k) {
+        for (size_t r = 0; r < NUM_OF_AMINO_ACIDS; ++r) {
+            match_scores_[r * M + k] = std::log(base_hmm.match_emissions[k][r] / kBackground[r]);  // MSV_HMM.cpp:38-45
+            if (inserts_) insert_scores_[r * M + k] = std::log(base_hmm.insert_emissions[k][r] / kBackground[r]);
+        }
+        for (size_t t = 0; t < NUM_OF_TRANSITIONS; ++t)
+            transition_scores_[k * NUM_OF_TRANSITIONS + t] = std::log(base_hmm.transitions[k][t]);
+    }
+    constexpr float nu = 2.0;  // the MSV path's specials, MSV_HMM.cpp:49-53
+    tr_B_Mk_ = std::log(2.0f / static_cast<float>(M * (M + 1)));
+    tr_E_C_ = std::log((nu - 1.0f) / nu);
+    tr_E_J_ = std::log(1.0f / nu);
+    check(msv_vit_profile_create(device, match_scores_.data(), inserts_ ? insert_scores_.data() : nullptr,
+                                 transition_scores_.data(), static_cast<uint32_t>(M), tr_B_Mk_, tr_E_C_, tr_E_J_,
+                                 &profile_),
+          "msv_vit_profile_create");
+}
+
+Viterbi_HMM::~Viterbi_HMM() { msv_vit_profile_destroy(profile_); }
+
+Viterbi_HMM::Viterbi_HMM(Viterbi_HMM&& o) noexcept
+    : viterbi_mu(o.viterbi_mu),
+      viterbi_lambda(o.viterbi_lambda),
+      model_length_(o.model_length_),
+      inserts_(o.inserts_),
+      match_scores_(std::move(o.match_scores_)),
+      insert_scores_(std::move(o.insert_scores_)),
+      transition_scores_(std::move(o.transition_scores_)),
+      tr_B_Mk_(o.tr_B_Mk_),
+      tr_E_C_(o.tr_E_C_),
+      tr_E_J_(o.tr_E_J_),
+      profile_(std::exchange(o.profile_, nullptr)) {}
+
+Viterbi_HMM& Viterbi_HMM::operator=(Viterbi_HMM&& o) noexcept {
+    if (this != &o) {
+        msv_vit_profile_destroy(profile_);
+        viterbi_mu = o.viterbi_mu;
+        viterbi_lambda = o.viterbi_lambda;
+        model_length_ = o.model_length_;
+        inserts_ = o.inserts_;
+        match_scores_ = std::move(o.match_scores_);
+        insert_scores_ = std::move(o.insert_scores_);
+        transition_scores_ = std::move(o.transition_scores_);
+        tr_B_Mk_ = o.tr_B_Mk_;
+        tr_E_C_ = o.tr_E_C_;
+        tr_E_J_ = o.tr_E_J_;
+        profile_ = std::exchange(o.profile_, nullptr);
+    }
+    return *this;
+}
+
+Log_score Viterbi_HMM::run_on_sequence(const Protein_sequence& seq) {
+    const size_t L = seq.empty() ? 0 : seq.size() - 1;
+    std::vector<uint8_t> codes(L);
+    if (L && msv_encode_residues(seq.data() + 1, L, codes.data()) != MSV_OK)
+        throw std::out_of_range("residue outside the 20 amino acids");
+    return msv_host::viterbi_run_on_sequence(match_scores_.data(), inserts_ ? insert_scores_.data() : nullptr,
+                                             transition_scores_.data(), model_length_, tr_B_Mk_, tr_E_C_, tr_E_J_,
+                                             codes.data(), L);
+}
+
+Log_score Viterbi_HMM::parallel_run_on_sequence(const Protein_sequence& seq) {
+    return score_batch(Protein_sequences{seq})[0];
+}
+
+std::vector<Log_score> Viterbi_HMM::score_batch(const Protein_sequences& seqs) {
+    return score_batch(Packed_sequences::pack(seqs));
+}
+
+std::vector<Log_score> Viterbi_HMM::score_batch(const Packed_sequences& packed) {
+    std::vector<Log_score> out(packed.size());
+    const msv_status s = msv_vit_score_batch(profile_, packed.codes.data(), packed.offsets.data(), packed.size(),
+                                             out.data(), nullptr);
+    if (s == MSV_ERR_BAD_RESIDUE) throw std::out_of_range("residue outside the 20 amino acids");
+    check(s, "msv_vit_score_batch");
+    return out;
+}
+
+Filter_result filter_pipeline(MSV_HMM& msv, Viterbi_HMM& vit, const Packed_sequences& packed, float msv_mu,
+                              float msv_lambda, double F1) {
+    Filter_result r;
+    const size_t n = packed.size();
+    r.msv_scores.resize(n);
+    r.passed.resize(n);
+    r.viterbi_scores.resize(n);
+    uint64_t passed = 0;
+    const msv_status s = msv_vit_filter_batch(msv.handle(), vit.handle(), packed.codes.data(), packed.offsets.data(),
+                                              n, msv_mu, msv_lambda, F1, r.msv_scores.data(), r.passed.data(),
+                                              r.viterbi_scores.data(), &passed);
+    if (s == MSV_ERR_BAD_RESIDUE) throw std::out_of_range("residue outside the 20 amino acids");
+    check(s, "msv_vit_filter_batch");
+    r.n_passed = static_cast<size_t>(passed);
+    return r;
+}

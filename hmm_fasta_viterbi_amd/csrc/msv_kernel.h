@@ -15,6 +15,10 @@ constexpr int kTableRows = 21;   // 20 residues + poison row
 constexpr int kWideBlocks = 64;
 constexpr int kLdsLimit = 163840;
 
+// Words per wave of the diagnostic stamps buffer (KernelArgs::stamps): realtime start/end, hwid|rows,
+// xcc|block, shader-clock start/end.
+constexpr int kStampWords = 6;
+
 constexpr uint32_t kErrBadResidue = 1u;
 constexpr uint32_t kErrTooLong = 2u;
 constexpr uint32_t kErrBadOrder = 4u;  // a dequeue-order entry >= n (caller's order, or a poisoned sort)

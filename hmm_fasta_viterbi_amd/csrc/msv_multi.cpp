@@ -13,6 +13,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <new>
 #include <thread>
 #include <vector>
@@ -97,12 +98,21 @@ struct DeviceGuard {
     }
 };
 
+// msv_debug_multi_no_alias: make pinned_alias fail, so the copy fallback below runs (tests).
+std::atomic<bool> g_no_alias{false};
+
 // Device alias of page-locked host residues (nullptr for pageable memory): every rank's kernel then
 // reads its shard in place over its own PCIe link instead of a staged copy (as msv_score_batch does).
+// Called with the rank's device current.  hipHostMalloc / hipHostRegister / torch pin_memory buffers are
+// portable (mapped into every device's address space: HIP allocates page-locked memory portable and
+// mapped on ROCm), so the call succeeds for any rank; if it fails anyway (a non-portable registration),
+// nullptr sends the shard through the copy path (enqueue_shard), which tests force with
+// msv_debug_multi_no_alias.
 const uint8_t* pinned_alias(const uint8_t* host) {
     hipPointerAttribute_t at{};
     void* h = const_cast<uint8_t*>(host);
-    if (!host || hipPointerGetAttributes(&at, h) != hipSuccess || at.type != hipMemoryTypeHost) {
+    if (!host || g_no_alias.load(std::memory_order_relaxed) || hipPointerGetAttributes(&at, h) != hipSuccess ||
+        at.type != hipMemoryTypeHost) {
         (void)hipGetLastError();
         return nullptr;
     }
@@ -157,6 +167,13 @@ msv_status enqueue_shard(Rank& r, const uint8_t* residues, const uint64_t* offse
 }  // namespace
 
 extern "C" {
+
+// Diagnostic (tests): on = every later msv_multi_score_batch copies page-locked shards instead of reading
+// them in place, as if the device alias were unavailable.  Not in msv.h.
+msv_status msv_debug_multi_no_alias(int on) {
+    g_no_alias.store(on != 0, std::memory_order_relaxed);
+    return MSV_OK;
+}
 
 void msv_multi_destroy(msv_multi* m) {
     if (!m) return;

@@ -2,8 +2,9 @@
 
 The library names its instantiations `msv_g<G>_s<S>[_a<SA>]_w<W>_p<PF>_d<D>` (csrc/msv_kernel.hip,
 MSV_VARIANT / MSV_SPLIT_VARIANT); the kernel is `msvk::msv_batch_kernel<G, S, W, PF, BIG, D, SA, RPFO>`,
-BIG = the table does not fit LDS (lds_rows_for < 21) and RPFO = 2 for the zero-copy twin that
-msv_score_batch runs on page-locked residues (0 for HBM-resident launches: bench.py's timed steps).
+BIG = the table does not fit LDS (lds_rows_for < 21) and RPFO the residue prefetch of the zero-copy twin
+that msv_score_batch runs on page-locked residues (0 for HBM-resident launches: bench.py's timed steps;
+zero_copy_rpfo mirrors msv_kernel_impl.h zc_fn).
 tools/rocprof_window.py and tools/pmc_summary.py filter dispatches on this exact symbol, and bench.py
 publishes PMC traffic only when the committed PMC file names the kernel its timed steps run.
 """
@@ -34,6 +35,20 @@ def parse_variant(name: str) -> dict:
     return {"G": g, "S": s, "SA": sa, "waves": w, "PF": p, "D": d, "BIG": big}
 
 
+def zero_copy_rpfo(v: dict) -> int:
+    """The RPFO of the instantiation a launch reading page-locked residues in place runs (msv_kernel_impl.h
+    zc_fn): 2 for 16/32-lane rows of more than 40 states (residues two rows ahead), kWideBlocks = 64 for
+    rows of up to 40 states with 16+ lanes and PF <= 2 (64-row superblocks; buffers of >= 64 bytes), and 0
+    -- no twin, the ordinary kernel -- for everything else (4/8-lane groups, whole-row rings, split,
+    BIG and two-stream variants)."""
+    plain = v["D"] == 1 and not v["BIG"] and v["SA"] == 0
+    if plain and v["G"] in (16, 32) and v["S"] > 40:
+        return 2
+    if plain and v["G"] >= 16 and v["S"] <= 40 and v["PF"] <= 2:
+        return 64
+    return 0
+
+
 def kernel_symbol(variant: str, zero_copy: bool = False) -> str:
     """`msv_batch_kernel<16, 88, 16, 2, false, 1, 0, 0>` for `msv_g16_s88_w16_p2_d1` (a substring of
     the demangled name rocprofv3 prints: `void msvk::msv_batch_kernel<...>(msvk::KernelArgs)`);
@@ -43,7 +58,7 @@ def kernel_symbol(variant: str, zero_copy: bool = False) -> str:
     if m:
         return f"msv_coop_kernel<{m.group(1)}, {m.group(2)}, {m.group(3) or m.group(2)}>"
     v = parse_variant(variant)
-    rpfo = 2 if zero_copy else 0
+    rpfo = zero_copy_rpfo(v) if zero_copy else 0
     big = "true" if v["BIG"] else "false"
     return (f"msv_batch_kernel<{v['G']}, {v['S']}, {v['waves']}, {v['PF']}, {big}, {v['D']}, {v['SA']}, "
             f"{rpfo}>")

@@ -4,6 +4,8 @@
 //   Profile_HMM               data_readers/Profile_HMM.hpp:21-49
 //   FASTA_protein_sequences   data_readers/FASTA_protein_sequences.hpp:9-14
 //   MSV_HMM                   algorithms/MSV_HMM.hpp:17-44
+//   Viterbi_HMM               (new) the Viterbi stage over the parts of Profile_HMM the
+//                             reference parses and never scores with (Profile_HMM.cpp:107-120)
 //
 // Differences from the reference, all deliberate:
 //   * errors throw (msv_error, or std::out_of_range for a residue outside the 20 amino acids,
@@ -153,3 +155,45 @@ class MSV_HMM::Multi_device {
   private:
     msv_multi* multi_ = nullptr;
 };
+
+// The Viterbi stage (recurrence and conventions in msv.h): HMMER3's generic local Viterbi over
+// the reference's parse -- insert emissions and the 7 transitions per node -- with the MSV path's specials.
+// Same shape as MSV_HMM: run_on_sequence is this library's serial CPU DP, parallel_run_on_sequence and
+// score_batch the gfx950 kernel (bit-identical to each other).  STATS LOCAL VITERBI gives the P-values.
+class Viterbi_HMM {
+  public:
+    explicit Viterbi_HMM(const Profile_HMM& base_hmm, int device = 0, msv_insert_mode inserts = MSV_INSERTS_ZERO);
+    ~Viterbi_HMM();
+    Viterbi_HMM(const Viterbi_HMM&) = delete;
+    Viterbi_HMM& operator=(const Viterbi_HMM&) = delete;
+    Viterbi_HMM(Viterbi_HMM&& o) noexcept;
+    Viterbi_HMM& operator=(Viterbi_HMM&& o) noexcept;
+
+    Log_score run_on_sequence(const Protein_sequence& seq);
+    Log_score parallel_run_on_sequence(const Protein_sequence& seq);
+    std::vector<Log_score> score_batch(const Protein_sequences& seqs);
+    std::vector<Log_score> score_batch(const Packed_sequences& packed);
+
+    msv_vit_profile* handle() { return profile_; }
+    size_t model_length() const { return model_length_; }
+    float viterbi_mu = 0, viterbi_lambda = 0;  // STATS LOCAL VITERBI (Profile_HMM.cpp:86-87)
+
+  private:
+    size_t model_length_ = 0;
+    bool inserts_ = false;
+    std::vector<float> match_scores_, insert_scores_, transition_scores_;  // [20][M], [20][M], [M][7]
+    float tr_B_Mk_ = 0, tr_E_C_ = 0, tr_E_J_ = 0;
+    msv_vit_profile* profile_ = nullptr;
+};
+
+// HMMER3's filter cascade on the GPU (msv_vit_filter_batch): MSV scores of every sequence, the survivors of
+// P <= F1 against (msv_mu, msv_lambda) -- a Profile_HMM's stats_local_msv_mu/lambda -- and their Viterbi
+// scores (-inf where a sequence did not pass).
+struct Filter_result {
+    std::vector<Log_score> msv_scores;
+    std::vector<uint8_t> passed;
+    std::vector<Log_score> viterbi_scores;
+    size_t n_passed = 0;
+};
+Filter_result filter_pipeline(MSV_HMM& msv, Viterbi_HMM& vit, const Packed_sequences& packed, float msv_mu,
+                              float msv_lambda, double F1 = 0.02);

@@ -112,7 +112,8 @@ int main(int argc, char** argv) {
             seqs.push_back(s);
         }
         for (const auto& kv : golden) {
-            auto m = MSV_HMM(Profile_HMM(root + "/data/profile_HMMs/" + kv.first));
+            const Profile_HMM prof(root + "/data/profile_HMMs/" + kv.first);
+            auto m = MSV_HMM(prof);
             auto par = m.score_batch(seqs);
             for (size_t i = 0; i < seqs.size(); ++i) {
                 const float seq = m.run_on_sequence(seqs[i]);
@@ -123,7 +124,41 @@ int main(int argc, char** argv) {
                 }
                 ++checked;
             }
+            // the Viterbi stage in the same shape: CPU DP vs the gfx950 kernel, both insert modes
+            for (msv_insert_mode mode : {MSV_INSERTS_ZERO, MSV_INSERTS_LOG_ODDS}) {
+                auto v = Viterbi_HMM(prof, 0, mode);
+                auto vpar = v.score_batch(seqs);
+                for (size_t i = 0; i < seqs.size(); ++i) {
+                    const float seq = v.run_on_sequence(seqs[i]);
+                    if (!same_bits(seq, vpar[i])) {
+                        std::printf("test_msv failed! Viterbi seq vs par %s (inserts %d) seq %zu: cpu %a, gpu %a\n",
+                                    kv.first.c_str(), static_cast<int>(mode), i, seq, vpar[i]);
+                        return 1;
+                    }
+                    ++checked;
+                }
+            }
         }
+    }
+    // the filter cascade: MSV -> P <= F1 -> Viterbi on the survivors, against the pieces one by one
+    {
+        const Profile_HMM prof(root + "/data/profile_HMMs/1400.hmm");
+        auto m = MSV_HMM(prof);
+        auto v = Viterbi_HMM(prof);
+        const Packed_sequences packed = Packed_sequences::pack(fasta.sequences);
+        const Filter_result r = filter_pipeline(m, v, packed, prof.stats_local_msv_mu, prof.stats_local_msv_lambda, 1.0);
+        const auto want_m = m.score_batch(packed);
+        const auto want_v = v.score_batch(packed);
+        for (size_t i = 0; i < packed.size(); ++i)
+            if (!same_bits(r.msv_scores[i], want_m[i]) || !r.passed[i] || !same_bits(r.viterbi_scores[i], want_v[i])) {
+                std::printf("test_msv failed! filter_pipeline seq %zu\n", i);
+                return 1;
+            }
+        if (r.n_passed != packed.size()) {
+            std::printf("test_msv failed! filter_pipeline F1 = 1 passed %zu of %zu\n", r.n_passed, packed.size());
+            return 1;
+        }
+        checked += static_cast<int>(2 * packed.size());
     }
     // one device through the RCCL multi-device context (1-rank communicator; the shard's scores take
     // the self send/recv path of the gather) equals one launch

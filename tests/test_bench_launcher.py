@@ -52,6 +52,15 @@ def test_kernel_symbols():
     from hmm_fasta_viterbi_amd.kernel_names import kernel_symbol
     assert kernel_symbol("msv_g16_s88_w16_p2_d1") == "msv_batch_kernel<16, 88, 16, 2, false, 1, 0, 0>"
     assert kernel_symbol("msv_g16_s88_w16_p2_d1", zero_copy=True).endswith(", 2>")
+    # zero-copy twins mirror msv_kernel_impl.h zc_fn: wide blocks for <= 40-state rows, none for 4/8 lanes,
+    # whole-row rings (PF > 2), split or BIG variants
+    assert kernel_symbol("msv_g16_s8_w4_p2_d1", zero_copy=True).endswith(", 0, 64>")
+    assert kernel_symbol("msv_g64_s8_w16_p2_d1", zero_copy=True).endswith(", 0, 64>")
+    assert kernel_symbol("msv_g64_s34_w16_p2_d1", zero_copy=True).endswith(", true, 1, 0, 0>")  # BIG
+    assert kernel_symbol("msv_g4_s28_w16_p2_d1", zero_copy=True).endswith(", 0, 0>")
+    assert kernel_symbol("msv_g16_s28_w16_p7_d1", zero_copy=True).endswith(", 0, 0>")
+    assert kernel_symbol("msv_g32_s76_a64_w16_p2_d1", zero_copy=True).endswith(", 64, 0>")
+    assert kernel_symbol("msv_g64_s48_w16_p2_d1", zero_copy=True).endswith(", 0, 0>")
     assert kernel_symbol("msv_g32_s76_a64_w16_p2_d1") == "msv_batch_kernel<32, 76, 16, 2, false, 1, 64, 0>"
     assert kernel_symbol("msv_g64_s48_w16_p2_d1") == "msv_batch_kernel<64, 48, 16, 2, true, 1, 0, 0>"
     assert kernel_symbol("msv_coop_w4_s6") == "msv_coop_kernel<4, 6, 6>"

@@ -314,9 +314,11 @@ def test_score_grid_random_fasta_and_seeded():
 
 
 def test_score_grid_fused_launch_matches_per_profile():
-    """A grid of few sequences runs as ONE launch over all profiles (each in the latency layout of the
-    largest model, msv_grid_kernel), in chunks of 32 profiles: 40 entries (all 24 profiles, 16 of them
-    twice) x 50 random + homolog sequences equal every profile's own launch bitwise, and the oracle."""
+    """A grid of few sequences runs as ONE launch over all profiles, in chunks of 32 profiles.  Here 32 x 50
+    workgroups per launch exceed the smallest profile's cooperative limit (coop_max_n), so the
+    launch takes the round-2 latency layout of the largest model (msv_grid_kernel, grid_fused): 40 entries
+    (all 24 profiles, 16 of them twice) x 50 random + homolog sequences equal every profile's own launch
+    bitwise, and the oracle."""
     rc, ro = random_batch(150, 40, 0, 900)
     hc, ho = homolog_batch(msv.Profile_HMM(profile_path("1400.hmm")).match_emissions, 151, 10, 1, 600)
     codes, offsets = concat_batches((rc, ro), (hc, ho))
@@ -329,6 +331,27 @@ def test_score_grid_fused_launch_matches_per_profile():
     for prof in ("100.hmm", "1400.hmm", "2405.hmm"):
         want = OracleProfile(prof).score_batch(codes, offsets)
         assert np.array_equal(bits(grid[names.index(prof)]), bits(want)), prof
+
+
+@pytest.mark.parametrize("coop_limit", [None, 0])
+def test_score_grid_small_grid_cooperative_or_latency_fused(coop_limit):
+    """benchmark_MSV's shape (every profile x 3 sequences, 72 workgroups per launch) runs the fused
+    cooperative grid (msv_coop_grid_kernel); with one profile's cooperative limit set to 0
+    (msv_debug_set_coop_max_n) the same grid takes the latency-layout fused launch (msv_grid_kernel) for
+    profiles of <= 2480 states.  Either way every score equals the profile's own launch and the golden."""
+    import ctypes as C
+    from hmm_fasta_viterbi_amd import _native
+    fa = msv.FASTA_protein_sequences(os.path.join(ROOT, "data", "FASTA_files", "random_FASTA.fsa"))
+    rows = read_golden_tsv("random_fasta_scores.tsv")
+    names = [p for p in PROFILES if int(p.split(".")[0]) <= 2480]
+    engines = [msv.MSV_HMM(msv.Profile_HMM(profile_path(p))) for p in names]
+    if coop_limit is not None:
+        _native.lib().msv_debug_set_coop_max_n.argtypes = [C.c_void_p, C.c_uint64]
+        _native.lib().msv_debug_set_coop_max_n(engines[3]._p, coop_limit)
+    grid = msv.score_grid(engines, fa.sequences)
+    for k, prof in enumerate(names):
+        want = np.array([w for p, i, L, w in rows if p == prof], np.float32)
+        assert np.array_equal(bits(grid[k]), bits(want)), (prof, coop_limit)
 
 
 @pytest.mark.parametrize("leng", [2600, 3500])

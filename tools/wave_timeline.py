@@ -11,6 +11,8 @@ import sys
 
 import numpy as np
 
+STAMP_WORDS = 6  # msv_kernel.h kStampWords: realtime start/end, hwid|rows, xcc|block, shader clock start/end
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -48,7 +50,7 @@ def main():
     s = torch.empty(n, dtype=torch.float32, device=dev)
     order = torch.empty(n, dtype=torch.int32, device=dev)
     nw = L.msv_debug_grid_waves(eng._p)
-    stamps = torch.zeros(nw * 4, dtype=torch.int64, device=dev)
+    stamps = torch.zeros(nw * STAMP_WORDS, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     if not args.no_order:
         eng.order_longest_first(o.data_ptr(), n, order.data_ptr(), st.cuda_stream)
@@ -58,7 +60,7 @@ def main():
     eng.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), n, s.data_ptr(), op, st.cuda_stream)
     eng.check(st.cuda_stream)
     L.msv_debug_set_stamps(eng._p, None)
-    a = stamps.cpu().numpy().reshape(nw, 4)
+    a = stamps.cpu().numpy().reshape(nw, STAMP_WORDS)
     a = a[a[:, 1] > 0]
     t0 = a[:, 0].min()
     start = (a[:, 0] - t0) / 100.0  # us
@@ -77,7 +79,7 @@ def main():
     W = eng.describe()["waves_per_block"]
     wid = np.zeros(len(a), int)
     # stamps are stored at index blockIdx*W + wave, recover wave-in-block from the row index
-    idx = np.nonzero(stamps.cpu().numpy().reshape(nw, 4)[:, 1] > 0)[0]
+    idx = np.nonzero(stamps.cpu().numpy().reshape(nw, STAMP_WORDS)[:, 1] > 0)[0]
     wid = idx % W
     res_extra = {
         "distinct_cus": int(len(waves_per_cu)),
@@ -91,6 +93,7 @@ def main():
         "launch_us": round(float(T), 1),
         "start_us_pct": q(start), "end_us_pct": q(end),
         "mean_wave_lifetime_frac": round(float(life.mean()), 4),
+        "clock_GHz": round(float((a[:, 5] - a[:, 4]).sum() / (a[:, 1] - a[:, 0]).sum() * 0.1), 4),
         "rows_per_wave_pct": q(rows),
         "ns_per_row_pct": q((end - start) * 1000.0 / np.maximum(rows, 1)),
         "waves_per_simd_pct": q(np.unique(cu_key * 4 + simd, return_counts=True)[1]),
