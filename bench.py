@@ -463,7 +463,7 @@ def main(args=None):
         assert hip.hipEventElapsedTime(C.byref(ms), a, b) == 0
         return float(ms.value)
 
-    native.msv_debug_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
+    native.msv_debug_set_clock_stamps.argtypes = [C.c_void_p, C.c_void_p]
     native.msv_debug_grid_waves.argtypes = [C.c_void_p]
 
     def step(ev=None, stamps=None):
@@ -473,8 +473,8 @@ def main(args=None):
             order_ptr = d_order.data_ptr()
         if ev is not None:  # the MSV launch itself updates these two HIP events (hipExtLaunchKernel)
             native.msv_debug_time_next_launch(engine._p, ev[0], ev[1])
-        if stamps is not None:  # ... and writes every wave's realtime / shader-clock stamps here
-            native.msv_debug_set_stamps(engine._p, stamps.data_ptr())
+        # stamps: this launch runs the plan's CLOCK twin, every wave writing realtime + shader-clock stamps
+        native.msv_debug_set_clock_stamps(engine._p, None if stamps is None else stamps.data_ptr())
         engine.score_batch_device(d_res.data_ptr(), residues, d_off.data_ptr(), n, d_scores.data_ptr(), order_ptr, sh)
         if gathered is not None and world > 1:  # cfg4: the RCCL gather of the scores is part of the step
             with torch.cuda.stream(stream):
@@ -567,36 +567,47 @@ def main(args=None):
     # the launch stream), not event records around it -- each record is a marker packet (~4 us in the
     # stream), which would add ~8 us to every step (7% of cfg2's).
     events = [(hip_event(), hip_event()) for _ in range(args.steps)]
-    # Clock during the timed steps: every wave of each timed launch stamps its start and end in realtime
-    # (100 MHz) and shader-clock ticks (s_memtime); clock = sum of ticks / sum of realtime over the waves
-    # (the kernel's existing diagnostic branch, taken once per wave at start and end).
-    nwaves = int(native.msv_debug_grid_waves(engine._p))
-    stamp_bufs = None if args.no_clock else [torch.zeros(nwaves * 6, dtype=torch.int64, device=dev)
-                                              for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(None if args.no_launch_events else events[k], None if stamp_bufs is None else stamp_bufs[k])
+        step(None if args.no_launch_events else events[k])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    native.msv_debug_set_stamps(engine._p, None)
     engine.check(sh)
+    # Clock under this load: `steps` more steps right after the timed window, the same batch and plan, run
+    # by the plan's CLOCK twin (msv_kernel_impl.h clock_fn: the production kernel whose per-wave stamps also
+    # record s_memtime -- one tick per shader cycle -- beside s_memrealtime at 100 MHz; a separate
+    # instantiation, so the timed kernel's ISA is untouched).  clock = sum of ticks / sum of realtime over
+    # the waves of a launch, median over the launches; the twin's own kernel time is reported beside it.
     clock = None
-    if stamp_bufs is not None:
+    if not args.no_clock:
+        nwaves = int(native.msv_debug_grid_waves(engine._p))
+        bufs = [torch.zeros(nwaves * 6, dtype=torch.int64, device=dev) for _ in range(args.steps)]
+        cev = [(hip_event(), hip_event()) for _ in range(args.steps)]
+        for k in range(args.steps):
+            step(cev[k], bufs[k])
+        native.msv_debug_set_clock_stamps(engine._p, None)
+        torch.cuda.synchronize(dev)
+        engine.check(sh)
         per_launch = []
-        for b in stamp_bufs:
+        for b in bufs:
             a = b.cpu().numpy().reshape(nwaves, 6)
-            a = a[a[:, 1] > 0]
+            a = a[(a[:, 1] > 0) & (a[:, 5] > 0)]
             rt, ck = (a[:, 1] - a[:, 0]).sum(), (a[:, 5] - a[:, 4]).sum()
             if rt > 0:
                 per_launch.append(float(ck) / float(rt) * 0.1)  # GHz
+        twin_ms = float(np.mean([hip_elapsed_ms(a, b) for a, b in cev]))
+        for a, b in cev:
+            hip.hipEventDestroy(a)
+            hip.hipEventDestroy(b)
         if per_launch:
             clock = {"median": round(float(np.median(per_launch)), 4), "min": round(float(min(per_launch)), 4),
-                     "max": round(float(max(per_launch)), 4), "launches": len(per_launch)}
+                     "max": round(float(max(per_launch)), 4), "launches": len(per_launch),
+                     "twin_kernel_ms": round(twin_ms, 4)}
     elapsed = t1 - t0
     kernel_ms = float("nan") if args.no_launch_events else float(np.mean([hip_elapsed_ms(a, b) for a, b in events]))
     for a, b in events:
@@ -702,9 +713,11 @@ def main(args=None):
                 "frac_at_clock": None if clock is None else round(
                     achieved / (256 * 128 * clock["median"] * 1e9 / 1e12), 4),
                 "clock": None if clock is None else {
-                    **clock, "source": "in-kernel: each timed launch's waves stamp s_memtime (one tick per shader "
-                                       "cycle) and s_memrealtime (100 MHz) at start and end; clock = sum of ticks / "
-                                       "sum of realtime over the waves, median over the timed launches; "
+                    **clock, "source": "in-kernel, over `steps` launches right after the timed window (same batch "
+                                       "and plan) by the plan's CLOCK twin, whose waves stamp s_memtime (one tick "
+                                       "per shader cycle) and s_memrealtime (100 MHz) at start and end; clock = sum "
+                                       "of ticks / sum of realtime over the waves, median over the launches; "
+                                       "twin_kernel_ms vs kernel_ms shows the twin ran like the timed kernel; "
                                        "frac_at_clock = achieved / (256 CU x 128 lanes x clock)"},
                 "traffic": traffic,
                 "traffic_source": traffic_src,

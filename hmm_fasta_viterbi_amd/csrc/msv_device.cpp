@@ -325,6 +325,7 @@ struct msv_profile {
     uint32_t* d_order = nullptr;  // msv_score_fasta_device's longest-first order
     size_t d_order_cap = 0;
     uint64_t* d_stamps = nullptr;  // diagnostic timeline buffer (tools only), or nullptr
+    bool stamp_clock = false;      // d_stamps is for the CLOCK twins (kStampWords per wave: bench.py clock_GHz)
     hipEvent_t time_start = nullptr, time_stop = nullptr;  // msv_debug_time_next_launch (one launch)
     hipEvent_t done = nullptr;     // grid API: joins this profile's stream back to the caller's
     hipStream_t shared = nullptr;  // shared_stream(device) once a host grid call used it
@@ -850,6 +851,18 @@ msv_status msv_profile_set_variant(msv_profile* p, const char* name) {
 msv_status msv_debug_set_stamps(msv_profile* p, uint64_t* d_stamps) {
     if (!p) return MSV_ERR_INVALID_ARGUMENT;
     p->d_stamps = d_stamps;
+    p->stamp_clock = false;
+    return MSV_OK;
+}
+
+// Diagnostics (bench.py roofline.clock_GHz), not in msv.h: subsequent launches of plans that have a CLOCK twin
+// (msv_kernel_impl.h clock_fn) run it and write msvk::kStampWords (6) uint64 per wave -- the 4 stamps above plus
+// shader-clock ticks (s_memtime) at the wave's start and end; launches of other plans write nothing.
+// nullptr switches it off.
+msv_status msv_debug_set_clock_stamps(msv_profile* p, uint64_t* d_stamps) {
+    if (!p) return MSV_ERR_INVALID_ARGUMENT;
+    p->d_stamps = d_stamps;
+    p->stamp_clock = d_stamps != nullptr;
     return MSV_OK;
 }
 
@@ -997,6 +1010,8 @@ static msv_status launch_batch(msv_profile* p, const uint8_t* d_residues, uint64
     a.tr_E_C = p->tr_E_C;
     a.tr_E_J = p->tr_E_J;
     a.stamps = p->d_stamps;
+    const bool clock = p->stamp_clock && !host_residues;
+    if (p->stamp_clock && (plan.cv || !plan.v->clock_fn || host_residues)) a.stamps = nullptr;  // no CLOCK twin
 
     const uint64_t want = (n + plan.groups_per_block - 1) / plan.groups_per_block;
     const int blocks = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(plan.blocks), want));
@@ -1025,7 +1040,7 @@ static msv_status launch_batch(msv_profile* p, const uint8_t* d_residues, uint64
     // to the buffer only from 4 bytes up: it takes buffers of at least 64 bytes
     const bool wide = plan.v->S <= 40;  // (twins of rows > 40 states prefetch two rows; see zc_fn)
     const bool twin = host_residues && (!wide || (p->zc_wide && residues_len >= 64));
-    MSV_HIP(msvk::launch_variant(*plan.v, dim3(blocks), a, st, t0, t1, twin));
+    MSV_HIP(msvk::launch_variant(*plan.v, dim3(blocks), a, st, t0, t1, twin, clock));
     p->kernels.dirty[k] = false;
     MSV_HIP(p->kernels.release(k, st, lazy_stream(p, st)));
     return MSV_OK;

@@ -16,8 +16,11 @@ constexpr int kWideBlocks = 64;
 constexpr int kLdsLimit = 163840;
 
 // Words per wave of the diagnostic stamps buffer (KernelArgs::stamps): realtime start/end, hwid|rows,
-// xcc|block, shader-clock start/end.
+// xcc|block (4 words in the production kernels), and in the CLOCK twins shader-clock (s_memtime) start/end.
 constexpr int kStampWords = 6;
+// RPFO value that selects a variant's CLOCK twin: the same kernel whose stamps also record shader-clock
+// ticks (bench.py's clock_GHz).  A separate instantiation, so the production kernels' ISA is untouched.
+constexpr int kClockTwin = -1;
 
 constexpr uint32_t kErrBadResidue = 1u;
 constexpr uint32_t kErrTooLong = 2u;
@@ -75,6 +78,7 @@ struct Variant {
     int sa = 0;  // split layout: states per lane staged in LDS (0 = whole table layout)
     const void* grid_fn = nullptr;  // msv_grid_kernel instantiation (G = 64 variants), else nullptr
     const void* zc_fn = nullptr;    // zero-copy twin (residues two rows ahead), else nullptr
+    const void* clock_fn = nullptr; // CLOCK twin (stamps record shader-clock ticks; bench configs' plans only)
 };
 
 const Variant* variants(int* count);
@@ -98,8 +102,10 @@ const CoopVariant* coop_variants(int* count);
 // timed launch costs no extra marker packets on the stream.
 // host_residues: args.residues is the device alias of page-locked host memory (the zero-copy twin
 // runs when the variant has one).
+// clock: run the variant's CLOCK twin (args.stamps set, kStampWords per wave); the caller checks clock_fn.
 hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, hipStream_t stream,
-                          hipEvent_t start = nullptr, hipEvent_t stop = nullptr, bool host_residues = false);
+                          hipEvent_t start = nullptr, hipEvent_t stop = nullptr, bool host_residues = false,
+                          bool clock = false);
 // Several profiles in one launch (v.grid_fn must be set).
 hipError_t launch_grid_variant(const Variant& v, const GridArgs& args, hipStream_t stream);
 hipError_t launch_pvalues(const float* scores, const uint64_t* offsets, uint64_t n, float mu, float lambda,

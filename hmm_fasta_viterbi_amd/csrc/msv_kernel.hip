@@ -234,9 +234,10 @@ const Variant* variants(int* count) {
 }
 
 hipError_t launch_variant(const Variant& v, dim3 grid, const KernelArgs& args, hipStream_t stream, hipEvent_t start,
-                          hipEvent_t stop, bool host_residues) {
+                          hipEvent_t stop, bool host_residues, bool clock) {
     void* params[] = {const_cast<KernelArgs*>(&args)};
     const void* fn = host_residues && v.zc_fn ? v.zc_fn : v.fn;
+    if (clock && v.clock_fn && !host_residues) fn = v.clock_fn;
     if (start || stop) return hipExtLaunchKernel(fn, grid, dim3(v.waves * 64), params, 0, stream, start, stop, 0);
     return hipLaunchKernel(fn, grid, dim3(v.waves * 64), params, 0, stream);
 }

@@ -224,6 +224,18 @@ constexpr const void* zc_fn() {
     else return nullptr;
 }
 
+// CLOCK twins (RPFO = kClockTwin): the plans bench.py's configs run -- 16 x 8 (cfg2), 16 x 88 (cfg3, cfg4),
+// the 32 x 76 split (cfg5) -- with stamps that also record s_memtime, for roofline.clock_GHz.  A separate
+// instantiation: adding the ticks to the production kernels renamed their registers and cost cfg2 1.3%
+// (profiles/r04_ab_stamp_clock.jsonl).
+template <int G, int S, int WAVES, int PF, bool BIG, int D, int SA = 0>
+constexpr const void* clock_fn() {
+    if constexpr (D == 1 && !BIG && PF == 2 &&
+                  ((G == 16 && (S == 8 || S == 88) && SA == 0) || (G == 32 && S == 76 && SA == 64)))
+        return reinterpret_cast<const void*>(&msv_batch_kernel<G, S, WAVES, PF, BIG, D, SA, kClockTwin>);
+    else return nullptr;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Variant table: every compiled (G, S, WAVES) instantiation.  The host picks the one whose G*S
 // covers LENG with the least estimated cost (the analog of the reference's should_specialize,
@@ -235,12 +247,14 @@ constexpr const void* zc_fn() {
                 &msv_batch_kernel<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_>),               \
             "msv_g" #G_ "_s" #S_ "_w" #W_ "_p" #P_ "_d" #D_, 0,                                              \
             grid_fn<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_>(),                            \
-            zc_fn<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_>()}
+            zc_fn<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_>(),                              \
+            clock_fn<G_, S_, W_, P_, (lds_rows_for(G_, S_) < kTableRows), D_>()}
 
 // Split layout (G = 32 or 64): SA states per lane from LDS (20 rows), S - SA from L2.
 #define MSV_SPLIT_VARIANT(G_, S_, SA_, W_, P_)                                                            \
     Variant{G_, S_, W_, P_, 1, kAminoAcids, false,                                                        \
             reinterpret_cast<const void*>(&msv_batch_kernel<G_, S_, W_, P_, false, 1, SA_>),               \
-            "msv_g" #G_ "_s" #S_ "_a" #SA_ "_w" #W_ "_p" #P_ "_d1", SA_, grid_fn<G_, S_, W_, P_, false, 1, SA_>()}
+            "msv_g" #G_ "_s" #S_ "_a" #SA_ "_w" #W_ "_p" #P_ "_d1", SA_, grid_fn<G_, S_, W_, P_, false, 1, SA_>(),  \
+            nullptr, clock_fn<G_, S_, W_, P_, false, 1, SA_>()}
 
 }  // namespace msvk

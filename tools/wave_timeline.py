@@ -11,7 +11,7 @@ import sys
 
 import numpy as np
 
-STAMP_WORDS = 6  # msv_kernel.h kStampWords: realtime start/end, hwid|rows, xcc|block, shader clock start/end
+STAMP_WORDS = 4  # msv_kernel_body.inc: realtime start/end, hwid|rows, xcc|block (production kernels)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -93,7 +93,6 @@ def main():
         "launch_us": round(float(T), 1),
         "start_us_pct": q(start), "end_us_pct": q(end),
         "mean_wave_lifetime_frac": round(float(life.mean()), 4),
-        "clock_GHz": round(float((a[:, 5] - a[:, 4]).sum() / (a[:, 1] - a[:, 0]).sum() * 0.1), 4),
         "rows_per_wave_pct": q(rows),
         "ns_per_row_pct": q((end - start) * 1000.0 / np.maximum(rows, 1)),
         "waves_per_simd_pct": q(np.unique(cu_key * 4 + simd, return_counts=True)[1]),
