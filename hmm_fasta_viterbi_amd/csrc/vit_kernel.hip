@@ -66,7 +66,9 @@ struct ChunkD {
 
 // PD > 0: a chunk's LDS/L2 data is requested PD chunks ahead and every chunk is its own scheduling region
 // (bounds the live loads: left alone, the scheduler hoists a whole row of loads and spills).
-template <int S, int NTREG, bool ELDS, bool ISC, int WAVES, int PD>
+// ASC: the row as ONE ascending pass (D chain interleaved with the M/I work) instead of a descending M/I pass
+// followed by an ascending D pass.
+template <int S, int NTREG, bool ELDS, bool ISC, int WAVES, int PD, bool ASC>
 __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
     static_assert(S >= 2 && S % 2 == 0, "S must be even");
     constexpr int C2 = S / 2;
@@ -186,61 +188,120 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                 sI = shift64(I[S - 1], sI);
                 sD = shift64(D[S - 1], sD);
 
-                // M/I pass, highest slot first: I(k) reads M'(k), I'(k) and M(k) reads M'(k-1), I'(k-1),
-                // D'(k-1), so every register is updated in place (no copies at the loop's back edge)
                 float E = NINF;
-                ChunkMI<NM> km[C2];
-                if constexpr (PD > 0) {
-#pragma unroll
-                    for (int c = C2 - 1; c >= 0 && c >= C2 - PD; --c) km[c] = load_mi(c);
-                }
-#pragma unroll
-                for (int c = C2 - 1; c >= 0; --c) {
+                if constexpr (ASC) {
+                    // ONE ascending pass: slot q's I and M read the previous row at q and q-1 (old values carried
+                    // in three registers) and its D the new M(q-1) and D(q-1), so the D chain runs interleaved
+                    // with the independent M/I work.  The lane's last M is made first (peeled) so it can cross
+                    // to the next lane for that lane's first D.
+                    const ChunkMI<NM> kl = load_mi(C2 - 1);
+                    const float mlast = fmaxf(fmaxf(M[S - 2] + Tm(kl, MM_IN, S - 1), I[S - 2] + Tm(kl, IM_IN, S - 1)),
+                                              fmaxf(D[S - 2] + Tm(kl, DM_IN, S - 1), Bt)) +
+                                        kl.e.y;
+                    sMn = shift64(mlast, sMn);
+                    ChunkMI<NM> km[C2];
+                    ChunkD<ND> kd[C2];
                     if constexpr (PD > 0) {
-                        if (c - PD >= 0) km[c - PD] = load_mi(c - PD);
-                    } else {
-                        km[c] = load_mi(c);
+#pragma unroll
+                        for (int c = 0; c < C2 && c < PD; ++c) {
+                            if (c < C2 - 1) km[c] = load_mi(c);
+                            if constexpr (ND > 0) kd[c] = load_d(c);
+                        }
                     }
-                    const ChunkMI<NM>& k = km[c];
+                    float pm = sM, pi = sI, pd = sD, mn = sMn, dn = NINF;
 #pragma unroll
-                    for (int h = 1; h >= 0; --h) {
-                        const int q = 2 * c + h;
-                        float iv = fmaxf(M[q] + Tm(k, MI, q), I[q] + Tm(k, II, q));
-                        if constexpr (ISC) iv = iv + (h ? k.i.y : k.i.x);
-                        const float pm = q ? M[q - 1] : sM, pi = q ? I[q - 1] : sI, pd = q ? D[q - 1] : sD;
-                        const float m = fmaxf(fmaxf(pm + Tm(k, MM_IN, q), pi + Tm(k, IM_IN, q)),
-                                              fmaxf(pd + Tm(k, DM_IN, q), Bt)) +
-                                        (h ? k.e.y : k.e.x);
-                        M[q] = m;
-                        I[q] = iv;
-                        E = fmaxf(E, m);
+                    for (int c = 0; c < C2; ++c) {
+                        if constexpr (PD > 0) {
+                            if (c + PD < C2) {
+                                if (c + PD < C2 - 1) km[c + PD] = load_mi(c + PD);
+                                if constexpr (ND > 0) kd[c + PD] = load_d(c + PD);
+                            }
+                        } else {
+                            if (c < C2 - 1) km[c] = load_mi(c);
+                            kd[c] = load_d(c);
+                        }
+                        const ChunkMI<NM>& k = c == C2 - 1 ? kl : km[c];
+                        const ChunkD<ND>& kdd = kd[c];
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int q = 2 * c + h;
+                            const float om = M[q], oi = I[q], od = D[q];
+                            float iv = fmaxf(om + Tm(k, MI, q), oi + Tm(k, II, q));
+                            if constexpr (ISC) iv = iv + (h ? k.i.y : k.i.x);
+                            const float m = q == S - 1 ? mlast
+                                                       : fmaxf(fmaxf(pm + Tm(k, MM_IN, q), pi + Tm(k, IM_IN, q)),
+                                                               fmaxf(pd + Tm(k, DM_IN, q), Bt)) +
+                                                             (h ? k.e.y : k.e.x);
+                            const float d = q ? fmaxf(mn + Td(kdd, MD_IN, q), dn + Td(kdd, DD_IN, q))
+                                              : mn + Td(kdd, MD_IN, 0);
+                            M[q] = m;
+                            I[q] = iv;
+                            D[q] = d;
+                            pm = om;
+                            pi = oi;
+                            pd = od;
+                            mn = m;
+                            dn = d;
+                            E = fmaxf(E, m);
+                        }
+                        if constexpr (PD > 0) __builtin_amdgcn_sched_barrier(0);
                     }
-                    if constexpr (PD > 0) __builtin_amdgcn_sched_barrier(0);
-                }
-                // this row's M(k-1) for each lane's first slot
-                sMn = shift64(M[S - 1], sMn);
-                // D pass, lowest slot first (the chain D(k) = max(M(k-1)+tMD, D(k-1)+tDD)), each lane's
-                // chain started from -inf; lazy-F below carries D across the lane boundaries
-                ChunkD<ND> kd[C2];
-                if constexpr (PD > 0 && ND > 0) {
-#pragma unroll
-                    for (int c = 0; c < C2 && c < PD; ++c) kd[c] = load_d(c);
-                }
-#pragma unroll
-                for (int c = 0; c < C2; ++c) {
+                } else {
+                    // M/I pass, highest slot first: I(k) reads M'(k), I'(k) and M(k) reads M'(k-1), I'(k-1),
+                    // D'(k-1), so every register is updated in place (no copies at the loop's back edge)
+                    ChunkMI<NM> km[C2];
+                    if constexpr (PD > 0) {
+    #pragma unroll
+                        for (int c = C2 - 1; c >= 0 && c >= C2 - PD; --c) km[c] = load_mi(c);
+                    }
+    #pragma unroll
+                    for (int c = C2 - 1; c >= 0; --c) {
+                        if constexpr (PD > 0) {
+                            if (c - PD >= 0) km[c - PD] = load_mi(c - PD);
+                        } else {
+                            km[c] = load_mi(c);
+                        }
+                        const ChunkMI<NM>& k = km[c];
+    #pragma unroll
+                        for (int h = 1; h >= 0; --h) {
+                            const int q = 2 * c + h;
+                            float iv = fmaxf(M[q] + Tm(k, MI, q), I[q] + Tm(k, II, q));
+                            if constexpr (ISC) iv = iv + (h ? k.i.y : k.i.x);
+                            const float pm = q ? M[q - 1] : sM, pi = q ? I[q - 1] : sI, pd = q ? D[q - 1] : sD;
+                            const float m = fmaxf(fmaxf(pm + Tm(k, MM_IN, q), pi + Tm(k, IM_IN, q)),
+                                                  fmaxf(pd + Tm(k, DM_IN, q), Bt)) +
+                                            (h ? k.e.y : k.e.x);
+                            M[q] = m;
+                            I[q] = iv;
+                            E = fmaxf(E, m);
+                        }
+                        if constexpr (PD > 0) __builtin_amdgcn_sched_barrier(0);
+                    }
+                    // this row's M(k-1) for each lane's first slot
+                    sMn = shift64(M[S - 1], sMn);
+                    // D pass, lowest slot first (the chain D(k) = max(M(k-1)+tMD, D(k-1)+tDD)), each lane's
+                    // chain started from -inf; lazy-F below carries D across the lane boundaries
+                    ChunkD<ND> kd[C2];
                     if constexpr (PD > 0 && ND > 0) {
-                        if (c + PD < C2) kd[c + PD] = load_d(c + PD);
-                    } else {
-                        kd[c] = load_d(c);
+    #pragma unroll
+                        for (int c = 0; c < C2 && c < PD; ++c) kd[c] = load_d(c);
                     }
-                    const ChunkD<ND>& k = kd[c];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int q = 2 * c + h;
-                        D[q] = q ? fmaxf(M[q - 1] + Td(k, MD_IN, q), D[q - 1] + Td(k, DD_IN, q))
-                                 : sMn + Td(k, MD_IN, 0);
+    #pragma unroll
+                    for (int c = 0; c < C2; ++c) {
+                        if constexpr (PD > 0 && ND > 0) {
+                            if (c + PD < C2) kd[c + PD] = load_d(c + PD);
+                        } else {
+                            kd[c] = load_d(c);
+                        }
+                        const ChunkD<ND>& k = kd[c];
+    #pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int q = 2 * c + h;
+                            D[q] = q ? fmaxf(M[q - 1] + Td(k, MD_IN, q), D[q - 1] + Td(k, DD_IN, q))
+                                     : sMn + Td(k, MD_IN, 0);
+                        }
+                        if constexpr (PD > 0 && ND > 0) __builtin_amdgcn_sched_barrier(0);
                     }
-                    if constexpr (PD > 0 && ND > 0) __builtin_amdgcn_sched_barrier(0);
                 }
                 // lazy-F: carry D across lane boundaries until no lane's first state changes
                 sDn = shift64(D[S - 1], sDn);
@@ -333,51 +394,58 @@ hipError_t launch_select(const float* scores, const uint64_t* offsets, uint64_t 
 // transitions move to LDS and match scores are read from L2 every row.  isc variants (insert_mode 1) read
 // insert scores from L2 and keep transitions in LDS.
 // ------------------------------------------------------------------------------------------------
-#define VIT_VARIANT(S_, NT_, ELDS_, ISC_, W_, PD_, NAME_)                                                \
+#define VIT_VARIANT(S_, NT_, ELDS_, ISC_, W_, PD_, ASC_, NAME_)                                        \
     VitVariant{S_,                                                                                       \
                NT_,                                                                                      \
                ELDS_,                                                                                    \
                ISC_,                                                                                     \
                W_,                                                                                       \
-               reinterpret_cast<const void*>(&vit_kernel<S_, NT_, ELDS_, ISC_, W_, PD_>),                 \
+               reinterpret_cast<const void*>(&vit_kernel<S_, NT_, ELDS_, ISC_, W_, PD_, ASC_>),          \
                NAME_,                                                                                    \
                (ELDS_ ? kRows * (S_)*kLanes * 4 : 0) + (kTransitions - (NT_)) * (S_)*kLanes * 4}
 
 const VitVariant* vit_variants(int* count) {
     static const VitVariant all[] = {
         // every transition array in VGPRs, match scores in LDS
-        VIT_VARIANT(2, 7, true, false, 8, 0, "vit_s2_t7"),
-        VIT_VARIANT(4, 7, true, false, 8, 0, "vit_s4_t7"),
-        VIT_VARIANT(6, 7, true, false, 8, 0, "vit_s6_t7"),
-        VIT_VARIANT(8, 7, true, false, 8, 0, "vit_s8_t7"),
-        VIT_VARIANT(10, 7, true, false, 8, 0, "vit_s10_t7"),
-        VIT_VARIANT(12, 7, true, false, 8, 0, "vit_s12_t7"),
-        VIT_VARIANT(14, 7, true, false, 8, 0, "vit_s14_t7"),
-        VIT_VARIANT(16, 7, true, false, 8, 0, "vit_s16_t7"),
-        VIT_VARIANT(18, 7, true, false, 8, 0, "vit_s18_t7"),
+        VIT_VARIANT(2, 7, true, false, 8, 0, false, "vit_s2_t7"),
+        VIT_VARIANT(4, 7, true, false, 8, 0, false, "vit_s4_t7"),
+        VIT_VARIANT(6, 7, true, false, 8, 0, false, "vit_s6_t7"),
+        VIT_VARIANT(8, 7, true, false, 8, 0, false, "vit_s8_t7"),
+        VIT_VARIANT(10, 7, true, false, 8, 0, false, "vit_s10_t7"),
+        VIT_VARIANT(12, 7, true, false, 8, 0, false, "vit_s12_t7"),
+        VIT_VARIANT(14, 7, true, false, 8, 0, false, "vit_s14_t7"),
+        VIT_VARIANT(16, 7, true, false, 8, 0, false, "vit_s16_t7"),
+        VIT_VARIANT(18, 7, true, false, 8, 0, false, "vit_s18_t7"),
         // five arrays in VGPRs, the D chain's two (MD, DD) in LDS
-        VIT_VARIANT(16, 5, true, false, 8, 1, "vit_s16_t5"),
-        VIT_VARIANT(18, 5, true, false, 8, 1, "vit_s18_t5"),
-        VIT_VARIANT(20, 5, true, false, 8, 1, "vit_s20_t5"),
-        VIT_VARIANT(22, 5, true, false, 8, 1, "vit_s22_t5"),
-        VIT_VARIANT(24, 5, true, false, 8, 1, "vit_s24_t5"),
+        VIT_VARIANT(16, 5, true, false, 8, 1, false, "vit_s16_t5"),
+        VIT_VARIANT(18, 5, true, false, 8, 1, false, "vit_s18_t5"),
+        VIT_VARIANT(20, 5, true, false, 8, 1, false, "vit_s20_t5"),
+        VIT_VARIANT(22, 5, true, false, 8, 1, false, "vit_s22_t5"),
+        VIT_VARIANT(24, 5, true, false, 8, 1, false, "vit_s24_t5"),
         // every transition array in LDS, match scores in LDS
-        VIT_VARIANT(16, 0, true, false, 8, 1, "vit_s16_t0"),
-        VIT_VARIANT(22, 0, true, false, 8, 1, "vit_s22_t0"),
+        VIT_VARIANT(16, 0, true, false, 8, 1, false, "vit_s16_t0"),
+        VIT_VARIANT(22, 0, true, false, 8, 1, false, "vit_s22_t0"),
         // transitions in LDS, match scores from L2
-        VIT_VARIANT(28, 0, false, false, 8, 3, "vit_s28_t0g"),
-        VIT_VARIANT(32, 0, false, false, 8, 3, "vit_s32_t0g"),
-        VIT_VARIANT(38, 0, false, false, 8, 3, "vit_s38_t0g"),
-        VIT_VARIANT(48, 0, false, false, 8, 3, "vit_s48_t0g"),
-        VIT_VARIANT(64, 0, false, false, 8, 3, "vit_s64_t0g"),
+        VIT_VARIANT(28, 0, false, false, 8, 3, false, "vit_s28_t0g"),
+        VIT_VARIANT(32, 0, false, false, 8, 3, false, "vit_s32_t0g"),
+        VIT_VARIANT(38, 0, false, false, 8, 3, false, "vit_s38_t0g"),
+        VIT_VARIANT(48, 0, false, false, 8, 3, false, "vit_s48_t0g"),
+        VIT_VARIANT(64, 0, false, false, 8, 3, false, "vit_s64_t0g"),
+        // the row as one ascending pass (D chain interleaved with the M/I work): A/B candidates
+        VIT_VARIANT(8, 7, true, false, 8, 0, true, "vit_s8_t7a"),
+        VIT_VARIANT(16, 7, true, false, 8, 0, true, "vit_s16_t7a"),
+        VIT_VARIANT(18, 7, true, false, 8, 0, true, "vit_s18_t7a"),
+        VIT_VARIANT(22, 5, true, false, 8, 1, true, "vit_s22_t5a"),
+        VIT_VARIANT(22, 0, true, false, 8, 1, true, "vit_s22_t0a"),
+        VIT_VARIANT(38, 0, false, false, 8, 3, true, "vit_s38_t0ga"),
         // informative insert scores (insert_mode 1): transitions in LDS, match and insert scores from L2
-        VIT_VARIANT(2, 0, false, true, 8, 3, "vit_s2_t0gi"),
-        VIT_VARIANT(8, 0, false, true, 8, 3, "vit_s8_t0gi"),
-        VIT_VARIANT(16, 0, false, true, 8, 3, "vit_s16_t0gi"),
-        VIT_VARIANT(22, 0, false, true, 8, 3, "vit_s22_t0gi"),
-        VIT_VARIANT(32, 0, false, true, 8, 3, "vit_s32_t0gi"),
-        VIT_VARIANT(38, 0, false, true, 8, 3, "vit_s38_t0gi"),
-        VIT_VARIANT(64, 0, false, true, 8, 3, "vit_s64_t0gi"),
+        VIT_VARIANT(2, 0, false, true, 8, 3, false, "vit_s2_t0gi"),
+        VIT_VARIANT(8, 0, false, true, 8, 3, false, "vit_s8_t0gi"),
+        VIT_VARIANT(16, 0, false, true, 8, 3, false, "vit_s16_t0gi"),
+        VIT_VARIANT(22, 0, false, true, 8, 3, false, "vit_s22_t0gi"),
+        VIT_VARIANT(32, 0, false, true, 8, 3, false, "vit_s32_t0gi"),
+        VIT_VARIANT(38, 0, false, true, 8, 3, false, "vit_s38_t0gi"),
+        VIT_VARIANT(64, 0, false, true, 8, 3, false, "vit_s64_t0gi"),
     };
     *count = static_cast<int>(sizeof(all) / sizeof(all[0]));
     return all;

@@ -5,7 +5,8 @@
 // Profile_HMM.cpp:10-11), the FASTA reader (the golden edge cases, first-line / EOF cases -- the
 // reference's sequences.back() on an empty vector, FASTA_protein_sequences.cpp:22 -- and a file large
 // enough for the multi-threaded chunked path), the precompute (MSV_HMM.cpp:35-57) and the CPU DP
-// (MSV_HMM.cpp:74-113) against the golden scores, and msv_shard_bounds.
+// (MSV_HMM.cpp:74-113) against the golden scores, msv_shard_bounds, and the Viterbi stage's table builder
+// and CPU DP (msv_hmm_viterbi_scores, msv_vit_cpu_score).
 // Usage: sanitize_host <repo_root>
 #include <dirent.h>
 #include <unistd.h>
@@ -267,6 +268,44 @@ int main(int argc, char** argv) {
         CHECK(msv_shard_bounds(nullptr, 0, 4, b.data()) == MSV_OK);
         for (uint64_t x : b) CHECK(x == 0);
         CHECK(msv_shard_bounds(off.data(), 6, 0, b.data()) == MSV_ERR_INVALID_ARGUMENT);
+    }
+
+    // 7. the Viterbi stage's host side: table builder + CPU DP on every profile, both insert
+    // modes, edge lengths; the MSV reduction (m->m = 1, every other transition impossible) equals the MSV DP
+    {
+        std::mt19937 rng(11);
+        for (const std::string& prof : profiles) {
+            msv_hmm* h = nullptr;
+            CHECK(msv_hmm_read((root + "/data/profile_HMMs/" + prof).c_str(), &h) == MSV_OK);
+            if (!h) continue;
+            const size_t M = msv_hmm_model_length(h);
+            std::vector<float> msc(20 * M), isc(20 * M), tsc(7 * M);
+            float b = 0, c = 0, j = 0;
+            for (int mode : {0, 1}) {
+                CHECK(msv_hmm_viterbi_scores(h, mode, msc.data(), isc.data(), tsc.data(), &b, &c, &j) == MSV_OK);
+                for (size_t L : {size_t(0), size_t(1), size_t(2), size_t(65), size_t(300)}) {
+                    std::vector<uint8_t> codes(L);
+                    for (auto& x : codes) x = static_cast<uint8_t>(rng() % 20);
+                    float sc = 0;
+                    CHECK(msv_vit_cpu_score(msc.data(), mode ? isc.data() : nullptr, tsc.data(), static_cast<uint32_t>(M),
+                                            b, c, j, codes.data(), L, &sc) == MSV_OK);
+                    CHECK(L > 0 ? std::isfinite(sc) : sc == -std::numeric_limits<float>::infinity());
+                }
+            }
+            std::vector<float> red(7 * M, -std::numeric_limits<float>::infinity());
+            for (size_t k = 0; k < M; ++k) red[k * 7] = 0.0f;
+            std::vector<uint8_t> codes(200);
+            for (auto& x : codes) x = static_cast<uint8_t>(rng() % 20);
+            float v = 0;
+            CHECK(msv_vit_cpu_score(msc.data(), nullptr, red.data(), static_cast<uint32_t>(M), b, c, j, codes.data(),
+                                    codes.size(), &v) == MSV_OK);
+            const float m = msv_host::run_on_sequence(msc.data(), M, b, c, j, codes.data(), codes.size());
+            CHECK(std::memcmp(&v, &m, sizeof(float)) == 0);
+            const uint8_t bad[3] = {1, 20, 2};
+            CHECK(msv_vit_cpu_score(msc.data(), nullptr, tsc.data(), static_cast<uint32_t>(M), b, c, j, bad, 3, &v) ==
+                  MSV_ERR_BAD_RESIDUE);
+            msv_hmm_destroy(h);
+        }
     }
 
     rmdir(dir.c_str());
