@@ -301,6 +301,30 @@ def viterbi_stage(args, msv_engine, prof_path, dev, stream, d_res, residues, d_o
     }
 
 
+def per_rank_summary(allr, steps: int, scaling: str) -> dict:
+    """Each rank's own figures for an N-rank line: allr = [world, 4] rows of {elapsed s,
+    kernel ms, residues, sequences} as all-gathered after the timed window; min / max / max-over-min of the
+    step time, kernel time and residues say whether a sub-linear curve is imbalance, the gather or launch skew."""
+    allr = np.asarray(allr, np.float64)
+
+    def spread(x):
+        x = np.asarray(x, np.float64)
+        return {"min": round(float(x.min()), 4), "max": round(float(x.max()), 4),
+                "max_over_min": round(float(x.max() / x.min()), 4) if x.min() > 0 else None}
+    step_ms = allr[:, 0] / steps * 1e3
+    return {
+        "ms_per_step": [round(float(v), 4) for v in step_ms],
+        "kernel_ms": [round(float(v), 4) for v in allr[:, 1]],
+        "residues": [int(v) for v in allr[:, 2]],
+        "sequences": [int(v) for v in allr[:, 3]],
+        "imbalance": {"ms_per_step": spread(step_ms), "kernel_ms": spread(allr[:, 1]), "residues": spread(allr[:, 2])},
+        "step_minus_kernel_ms": [round(float(a - b), 4) for a, b in zip(step_ms, allr[:, 1])],
+        "note": "each rank's own timed window (barrier-bracketed); `ms_per_step` and `kernel_ms` above are the "
+                "max over ranks; a step's time beyond its kernel (step_minus_kernel_ms) is the order launch"
+                + (" and the in-step RCCL all-gather" if scaling == "strong" else ""),
+    }
+
+
 def pmc_traffic(config: str, variant: str):
     """HBM bytes per launch from the committed rocprofv3 --pmc passes (profiles/pmc_<config>.json,
     tools/pmc.sh -> tools/pmc_summary.py), FETCH_SIZE corrected by the factor measured for the
@@ -624,22 +648,7 @@ def main(args=None):
         allr = allr.cpu().numpy().reshape(world, 4)
         elapsed, kernel_ms = float(allr[:, 0].max()), float(allr[:, 1].max())
         residues_all = int(allr[:, 2].sum())
-
-        def spread(x):
-            x = np.asarray(x, np.float64)
-            return {"min": round(float(x.min()), 4), "max": round(float(x.max()), 4),
-                    "max_over_min": round(float(x.max() / x.min()), 4) if x.min() > 0 else None}
-        per_rank = {
-            "ms_per_step": [round(float(v) / args.steps * 1e3, 4) for v in allr[:, 0]],
-            "kernel_ms": [round(float(v), 4) for v in allr[:, 1]],
-            "residues": [int(v) for v in allr[:, 2]],
-            "sequences": [int(v) for v in allr[:, 3]],
-            "imbalance": {"ms_per_step": spread(allr[:, 0] / args.steps * 1e3), "kernel_ms": spread(allr[:, 1]),
-                          "residues": spread(allr[:, 2])},
-            "note": "each rank's own timed window (barrier-bracketed); `ms_per_step` and `kernel_ms` above are "
-                    "the max over ranks; a step's time beyond its kernel is the order launch"
-                    + (" and the in-step RCCL all-gather" if scaling == "strong" else ""),
-        }
+        per_rank = per_rank_summary(allr, args.steps, scaling)
 
     # weak configs: output collection after timing (RCCL all-gather of every rank's scores)
     gather_ms = None

@@ -67,3 +67,18 @@ def test_kernel_symbols():
     assert kernel_symbol("msv_coop_w4_s10_a6") == "msv_coop_kernel<4, 10, 6>"
     with pytest.raises(ValueError):
         kernel_symbol("not_a_variant")
+
+
+def test_per_rank_summary():
+    """The N-rank line's per-rank block (bench.py per_rank_summary): each rank's step and kernel time, residues,
+    and the max-over-min imbalance of each."""
+    import numpy as np
+    from bench import per_rank_summary
+    allr = np.array([[0.060, 2.80, 40_000_000, 100_000], [0.063, 2.95, 41_000_000, 100_000]])
+    d = per_rank_summary(allr, 20, "strong")
+    assert d["ms_per_step"] == [3.0, 3.15] and d["kernel_ms"] == [2.8, 2.95]
+    assert d["residues"] == [40_000_000, 41_000_000] and d["sequences"] == [100_000, 100_000]
+    assert d["imbalance"]["residues"]["max_over_min"] == round(41 / 40, 4)
+    assert d["imbalance"]["kernel_ms"]["max"] == 2.95 and d["step_minus_kernel_ms"] == [0.2, 0.2]
+    assert "all-gather" in d["note"]
+
