@@ -103,11 +103,11 @@ std::atomic<bool> g_no_alias{false};
 
 // Device alias of page-locked host residues (nullptr for pageable memory): every rank's kernel then
 // reads its shard in place over its own PCIe link instead of a staged copy (as msv_score_batch does).
-// Called with the rank's device current.  hipHostMalloc / hipHostRegister / torch pin_memory buffers are
-// portable (mapped into every device's address space: HIP allocates page-locked memory portable and
-// mapped on ROCm), so the call succeeds for any rank; if it fails anyway (a non-portable registration),
-// nullptr sends the shard through the copy path (enqueue_shard), which tests force with
-// msv_debug_multi_no_alias.
+// Called with the rank's device current.  ROCm documents hipHostMallocPortable as its default behaviour
+// (page-locked memory is registered for every device), which covers msv_host_alloc and torch pin_memory;
+// whether a non-owning device gets an alias has only run on one-GPU boxes here, so it is not relied on:
+// when the call fails, nullptr sends the shard through the copy path (enqueue_shard), which
+// msv_debug_multi_no_alias forces in the GPU tests (bitwise against one launch).
 const uint8_t* pinned_alias(const uint8_t* host) {
     hipPointerAttribute_t at{};
     void* h = const_cast<uint8_t*>(host);

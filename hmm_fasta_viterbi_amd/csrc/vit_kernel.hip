@@ -71,6 +71,10 @@ struct ChunkD {
 template <int S, int NTREG, bool ELDS, bool ISC, int WAVES, int PD, bool ASC>
 __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
     static_assert(S >= 2 && S % 2 == 0, "S must be even");
+    // Rows two per loop trip where the registers allow it (the copies at a one-row loop's back edge); the
+    // long rows of the L2 variants (S > 24) keep one row per trip: two rows' register assignments did not
+    // fit 256 VGPRs there (S = 38: 83-124 spilled VGPRs).
+    constexpr bool TWO_ROWS = S <= 24;
     constexpr int C2 = S / 2;
     constexpr int ROW2 = C2 * kLanes;                     // float2 per table row
     constexpr int NTL = kTransitions - NTREG;             // transition arrays in LDS
@@ -323,11 +327,13 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                 if (wave_any(J >= N)) B = fmaxf(N, msvk::group_max<64>(J)) + move;
             };
             uint64_t i = 0;
-            for (; i + 1 < L; i += 2) {
-                row(i);
-                row(i + 1);
+            if constexpr (TWO_ROWS) {
+                for (; i + 1 < L; i += 2) {
+                    row(i);
+                    row(i + 1);
+                }
             }
-            if (i < L) row(i);
+            for (; i < L; ++i) row(i);
             const float sc = msvk::group_max<64>(Cp) + move;
             if (lane == 0) {
                 if (maxcode >= 20u) {
