@@ -444,6 +444,10 @@ const VitVariant* vit_variants(int* count) {
         VIT_VARIANT(22, 5, true, false, 8, 1, true, "vit_s22_t5a"),
         VIT_VARIANT(22, 0, true, false, 8, 1, true, "vit_s22_t0a"),
         VIT_VARIANT(38, 0, false, false, 8, 3, true, "vit_s38_t0ga"),
+        // one wave per SIMD (4 per workgroup): the 512-register budget holds S = 38 without the 52 spilled
+        // VGPRs of the 8-wave form (S = 48: 12 instead of 169): A/B candidates
+        VIT_VARIANT(38, 0, false, false, 4, 1, false, "vit_s38_t0g4"),
+        VIT_VARIANT(48, 0, false, false, 4, 3, false, "vit_s48_t0g4"),
         // informative insert scores (insert_mode 1): transitions in LDS, match and insert scores from L2
         VIT_VARIANT(2, 0, false, true, 8, 3, false, "vit_s2_t0gi"),
         VIT_VARIANT(8, 0, false, true, 8, 3, false, "vit_s8_t0gi"),
