@@ -448,6 +448,14 @@ const VitVariant* vit_variants(int* count) {
         // VGPRs of the 8-wave form (S = 48: 12 instead of 169): A/B candidates
         VIT_VARIANT(38, 0, false, false, 4, 1, false, "vit_s38_t0g4"),
         VIT_VARIANT(48, 0, false, false, 4, 3, false, "vit_s48_t0g4"),
+        // one wave per SIMD with every transition array in registers (no transition reads from LDS)
+        VIT_VARIANT(16, 7, true, false, 4, 0, false, "vit_s16_t7w4"),
+        VIT_VARIANT(22, 7, true, false, 4, 0, false, "vit_s22_t7w4"),
+        VIT_VARIANT(22, 7, true, false, 4, 0, true, "vit_s22_t7w4a"),
+        VIT_VARIANT(24, 7, true, false, 4, 0, false, "vit_s24_t7w4"),
+        VIT_VARIANT(28, 7, true, false, 4, 0, false, "vit_s28_t7w4"),
+        VIT_VARIANT(38, 7, false, false, 4, 3, false, "vit_s38_t7gw4"),
+        VIT_VARIANT(48, 7, false, false, 4, 3, false, "vit_s48_t7gw4"),
         // informative insert scores (insert_mode 1): transitions in LDS, match and insert scores from L2
         VIT_VARIANT(2, 0, false, true, 8, 3, false, "vit_s2_t0gi"),
         VIT_VARIANT(8, 0, false, true, 8, 3, false, "vit_s8_t0gi"),

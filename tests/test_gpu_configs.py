@@ -14,6 +14,7 @@ whole batch.
   cfg5: 2405.hmm x 100,000 sequences, len U[1500,2500], seed 4 -- the host path equals one launch,
         permutation invariance, and EVERY score equals the oracle's (~4.8e11 cells).
 """
+import ctypes as C
 import os
 
 import numpy as np
