@@ -185,10 +185,11 @@ def cpu_baseline(profile_path, codes, offsets, gpu_scores, target_s, threads):
 VIT_OPS_PER_CELL = 14  # fp32 ops per Viterbi DP cell (msv.h): M 3 adds + 3 max + 1 add, I 2 + 1, D 2 + 1, E 1
 
 
-def viterbi_stage(args, msv_engine, prof_path, dev, stream, d_res, residues, d_off, n, d_scores, codes, offsets,
-                  lmax, leng, hip_event, hip_elapsed_ms, F1=0.02):
+def viterbi_stage(args, msv_engine, prof_path, dev, stream, d_res, residues, d_off, n, d_scores, d_order, codes,
+                  offsets, lmax, leng, hip_event, hip_elapsed_ms, F1=0.02):
     """Information, never `value`: the Viterbi stage on this batch's MSV survivors.  The
-    timed steps' device scores -> msv_filter_select_device (P <= F1 against STATS LOCAL MSV, on the GPU)
+    timed steps' device scores -> msv_filter_select_device (P <= F1 against STATS LOCAL MSV, on the GPU,
+    survivors listed in the MSV launch's longest-first order)
     -> ONE Viterbi launch over the survivors list (count read on the device), timed with HIP events the
     launch itself updates.  Roofline: 14 fp32 add/max ops per cell (cells = survivor residues x LENG).
     CPU baseline: the oracle's serial Viterbi ("port") on a bounded sample of the survivors, on the host
@@ -207,7 +208,8 @@ def viterbi_stage(args, msv_engine, prof_path, dev, stream, d_res, residues, d_o
     d_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     d_vsc = torch.full((max(n, 1),), float("-inf"), dtype=torch.float32, device=dev)
     from hmm_fasta_viterbi_amd._native import check
-    check(native.msv_filter_select_device(dev.index or 0, d_scores.data_ptr(), d_off.data_ptr(), n, msv_engine.msv_mu,
+    check(native.msv_filter_select_device(dev.index or 0, d_scores.data_ptr(), d_off.data_ptr(),
+                                          None if d_order is None else d_order.data_ptr(), n, msv_engine.msv_mu,
                                           msv_engine.msv_lambda, F1, None, d_sel.data_ptr(), d_cnt.data_ptr(), sh))
 
     def launch(ev=None):
@@ -773,7 +775,8 @@ def main(args=None):
         }
         if not args.no_viterbi:
             result["viterbi_stage"] = viterbi_stage(args, engine, prof_path, dev, stream, d_res, residues, d_off, n,
-                                                    d_scores, codes, offsets, lmax, leng, hip_event, hip_elapsed_ms)
+                                                    d_scores, None if args.no_order else d_order, codes, offsets,
+                                                    lmax, leng, hip_event, hip_elapsed_ms)
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(prof_path, codes, offsets, scores, args.cpu_seconds,
                                                   cpu_threads(args.cpu_threads))

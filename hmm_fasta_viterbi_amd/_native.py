@@ -200,7 +200,7 @@ def lib() -> C.CDLL:
         "msv_score_fasta_device": (C.c_int, [vp, vp, vp]),
         "msv_score_batch_multi": (C.c_int, [vp, C.c_uint32, vp, vp, u64, vp]),
         "msv_pvalues_device": (C.c_int, [C.c_int, vp, vp, u64, C.c_float, C.c_float, vp, vp]),
-        "msv_filter_select_device": (C.c_int, [C.c_int, vp, vp, u64, f32, f32, C.c_double, vp, vp, vp, vp]),
+        "msv_filter_select_device": (C.c_int, [C.c_int, vp, vp, vp, u64, f32, f32, C.c_double, vp, vp, vp, vp]),
         "msv_hmm_viterbi_scores": (C.c_int, [vp, C.c_int, vp, vp, vp, fp, fp, fp]),
         "msv_vit_cpu_score": (C.c_int, [vp, vp, vp, u32, f32, f32, f32, vp, u64, fp]),
         "msv_vit_profile_create": (C.c_int, [C.c_int, vp, vp, vp, u32, f32, f32, f32, C.POINTER(vp)]),

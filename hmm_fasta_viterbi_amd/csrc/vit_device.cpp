@@ -432,9 +432,9 @@ msv_status msv_vit_score_batch(msv_vit_profile* p, const uint8_t* residues, cons
     return msv_vit_profile_check(p, st);
 }
 
-msv_status msv_filter_select_device(int device, const float* d_scores, const uint64_t* d_offsets, uint64_t n,
-                                    float mu, float lambda, double threshold, double* d_pvalues,
-                                    uint32_t* d_selected, uint32_t* d_count, void* stream) {
+msv_status msv_filter_select_device(int device, const float* d_scores, const uint64_t* d_offsets,
+                                    const uint32_t* d_order, uint64_t n, float mu, float lambda, double threshold,
+                                    double* d_pvalues, uint32_t* d_selected, uint32_t* d_count, void* stream) {
     if (!d_count || (n && (!d_scores || !d_offsets || !d_selected))) return MSV_ERR_INVALID_ARGUMENT;
     if (n >= (1ull << 32)) return MSV_ERR_INVALID_ARGUMENT;
     Guard g(device);
@@ -442,7 +442,7 @@ msv_status msv_filter_select_device(int device, const float* d_scores, const uin
     hipStream_t st = static_cast<hipStream_t>(stream);
     VIT_HIP(hipMemsetAsync(d_count, 0, sizeof(uint32_t), st));
     return hip_status(
-        vitk::launch_select(d_scores, d_offsets, n, mu, lambda, threshold, d_pvalues, d_selected, d_count, st));
+        vitk::launch_select(d_scores, d_offsets, d_order, n, mu, lambda, threshold, d_pvalues, d_selected, d_count, st));
 }
 
 msv_status msv_vit_filter_batch(msv_profile* msv, msv_vit_profile* vit, const uint8_t* residues,
@@ -487,8 +487,9 @@ msv_status msv_vit_filter_batch(msv_profile* msv, msv_vit_profile* vit, const ui
     // survivors (P <= F1) -> Viterbi, all on the device; non-survivors keep -inf
     std::vector<float> ninf(n, kNinf);
     VIT_HIP(hipMemcpyAsync(vit->d_sc, ninf.data(), n * sizeof(float), hipMemcpyHostToDevice, st));
-    if ((s = msv_filter_select_device(vit->device, vit->d_msc_out, vit->d_off, n, msv_mu, msv_lambda, F1, nullptr,
-                                      vit->d_sel, vit->d_words + 3, st)) != MSV_OK)
+    // survivors listed longest first (the MSV launch's order): the Viterbi launch's tail is its shortest ones
+    if ((s = msv_filter_select_device(vit->device, vit->d_msc_out, vit->d_off, vit->d_ord, n, msv_mu, msv_lambda, F1,
+                                      nullptr, vit->d_sel, vit->d_words + 3, st)) != MSV_OK)
         return s;
     if ((s = launch(vit, vit->d_res, vit->d_off, n, vit->d_sel, vit->d_words + 3, vit->d_sc, st)) != MSV_OK) return s;
     uint32_t count = 0;

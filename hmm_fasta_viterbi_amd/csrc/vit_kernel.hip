@@ -363,12 +363,15 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
 // one atomic per wave.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void vit_select_kernel(const float* __restrict__ scores,
-                                                         const uint64_t* __restrict__ offsets, uint64_t n, float mu,
+                                                         const uint64_t* __restrict__ offsets,
+                                                         const uint32_t* __restrict__ order, uint64_t n, float mu,
                                                          float lambda, double threshold, double* __restrict__ pvalues,
                                                          uint32_t* __restrict__ select, uint32_t* __restrict__ count) {
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t pos = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     bool pass = false;
-    if (i < n) {
+    uint64_t i = pos;
+    if (pos < n) {
+        if (order) i = order[pos];  // (a permutation: every sequence is visited once)
         const double p = msvk::msv_pvalue_of(scores[i], offsets[i + 1] - offsets[i], mu, lambda);
         if (pvalues) pvalues[i] = p;
         pass = p <= threshold;
@@ -384,13 +387,14 @@ __global__ __launch_bounds__(256) void vit_select_kernel(const float* __restrict
     if (pass) select[base + below] = static_cast<uint32_t>(i);
 }
 
-hipError_t launch_select(const float* scores, const uint64_t* offsets, uint64_t n, float mu, float lambda,
-                         double threshold, double* pvalues, uint32_t* select, uint32_t* count, hipStream_t stream) {
+hipError_t launch_select(const float* scores, const uint64_t* offsets, const uint32_t* order, uint64_t n, float mu,
+                         float lambda, double threshold, double* pvalues, uint32_t* select, uint32_t* count,
+                         hipStream_t stream) {
     const uint64_t blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     if (blocks == 0) return hipSuccess;
     hipLaunchKernelGGL(vit_select_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream, scores, offsets,
-                       n, mu, lambda, threshold, pvalues, select, count);
+                       order, n, mu, lambda, threshold, pvalues, select, count);
     return hipGetLastError();
 }
 

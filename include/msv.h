@@ -300,11 +300,14 @@ msv_status msv_pvalues_device(int device, const float* d_scores, const uint64_t*
 
 /* MSV filter on the device: the P-value of every score (the formula above, written to d_pvalues when it
  * is not NULL) and the indices of the sequences with P <= threshold appended to d_selected (n uint32 of
- * room; their order is arbitrary), their number in *d_count (one device uint32, zeroed here first).
- * The survivors list feeds msv_vit_score_batch_device directly (no host round trip). */
-msv_status msv_filter_select_device(int device, const float* d_scores, const uint64_t* d_offsets, uint64_t n,
-                                    float mu, float lambda, double threshold, double* d_pvalues,
-                                    uint32_t* d_selected, uint32_t* d_count, void* stream);
+ * room), their number in *d_count (one device uint32, zeroed here first).  d_order (NULL or a permutation
+ * of 0..n-1, e.g. msv_order_longest_first's) is the order the survivors are listed in, up to the order in
+ * which 64-entry stretches of it append (one atomic per stretch): with the longest-first permutation the
+ * Viterbi launch dequeues its longest survivors first.  The survivors list feeds
+ * msv_vit_score_batch_device directly (no host round trip). */
+msv_status msv_filter_select_device(int device, const float* d_scores, const uint64_t* d_offsets,
+                                    const uint32_t* d_order, uint64_t n, float mu, float lambda, double threshold,
+                                    double* d_pvalues, uint32_t* d_selected, uint32_t* d_count, void* stream);
 
 /* ---- Viterbi stage -----------------------------------------------------------
  * The reference parses everything a Viterbi filter needs -- insert_emissions and the 7 transitions

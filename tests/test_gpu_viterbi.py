@@ -196,6 +196,51 @@ def test_select_list_and_device_count():
     assert np.all(got[~mask] == 7.0)
 
 
+def test_filter_select_device_order():
+    """msv_filter_select_device: the survivors (P <= F1) equal the host formula's mask, with or without a
+    dequeue order; with msv_order_longest_first's permutation every 64-entry stretch of it appends as one
+    contiguous run in order (one atomic per stretch), so the Viterbi launch takes its longest survivors first."""
+    import torch
+    from hmm_fasta_viterbi_amd import _native
+    prof = "1400.hmm"
+    m = msv.MSV_HMM(hmm(prof))
+    codes, offsets = mixed_batch(prof, 91, 1500, 50, 900)
+    n = len(offsets) - 1
+    sc = OracleProfile(prof).score_batch(codes, offsets, threads=8)
+    F1 = 0.05
+    want = np.nonzero(m.pvalues(sc, offsets) <= F1)[0]
+    assert 0 < len(want) < n
+    dev = torch.device("cuda:0")
+    d_sc = torch.from_numpy(sc).to(dev)
+    d_off = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    d_ord = torch.empty(n, dtype=torch.int32, device=dev)
+    d_sel = torch.empty(n, dtype=torch.int32, device=dev)
+    d_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    st = torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    m.order_longest_first(d_off.data_ptr(), n, d_ord.data_ptr(), st.cuda_stream)
+    L = _native.lib()
+    for order in (None, d_ord.data_ptr()):
+        _native.check(L.msv_filter_select_device(0, d_sc.data_ptr(), d_off.data_ptr(), order, n, m.msv_mu,
+                                                 m.msv_lambda, F1, None, d_sel.data_ptr(), d_cnt.data_ptr(),
+                                                 st.cuda_stream))
+        st.synchronize()
+        cnt = int(d_cnt.item())
+        got = d_sel[:cnt].cpu().numpy().view(np.uint32).astype(np.int64)
+        assert cnt == len(want) and np.array_equal(np.sort(got), want)
+        if order is not None:
+            pos = np.empty(n, np.int64)
+            pos[d_ord.cpu().numpy().astype(np.int64)] = np.arange(n)
+            p = pos[got]
+            stretch = p // 64
+            starts = np.r_[True, stretch[1:] != stretch[:-1]]
+            assert len(np.unique(stretch)) == int(starts.sum())  # each stretch one contiguous run ...
+            same = ~starts[1:]
+            assert np.all(p[1:][same] > p[:-1][same])  # ... in the order's order
+            lens = np.diff(offsets.astype(np.int64))
+            assert np.all(np.diff(lens[d_ord.cpu().numpy().astype(np.int64)]) <= 0)  # the order is longest first
+
+
 def test_filter_pipeline_matches_composition():
     """msv_vit_filter_batch (MSV -> P <= F1 -> Viterbi, on the device) = the oracle's MSV scores, the host
     P-value formula's pass mask, and the oracle's Viterbi scores on exactly those sequences."""

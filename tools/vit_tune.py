@@ -2,7 +2,7 @@
 rounds in one process, and check that they agree bitwise.  The batch: the MSV filter's survivors (P <= F1)
 of bench.py's rank-0 batch of a config (--config), or --n random sequences.
 
-    python tools/vit_tune.py --config cfg3 [--variants a,b] [--rounds 3]
+    python tools/vit_tune.py --config cfg3 [--variants a,b] [--rounds 3] [--longest-first]
     python tools/vit_tune.py --profile 2405.hmm --n 2000 --lmin 1500 --lmax 2500
 """
 import argparse
@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="")
     ap.add_argument("--insert-mode", type=int, default=0)
+    ap.add_argument("--longest-first", action="store_true",
+                    help="survivors listed longest first (as msv_filter_select_device with the MSV order lists them)")
     a = ap.parse_args()
     import torch
     import hmm_fasta_viterbi_amd as msv
@@ -57,6 +59,8 @@ def main():
         m = msv.MSV_HMM(h)
         sc = m.score_batch(codes=codes, offsets=offsets)
         keep = np.nonzero(m.pvalues(sc, offsets) <= a.F1)[0]
+        if a.longest_first:
+            keep = keep[np.argsort(-np.diff(offsets.astype(np.int64))[keep], kind="stable")]
         parts = [codes[int(offsets[i]):int(offsets[i + 1])] for i in keep]
         offs = np.zeros(len(keep) + 1, np.uint64)
         np.cumsum([len(p) for p in parts], out=offs[1:])
@@ -106,7 +110,8 @@ def main():
         info = None
         vit.set_variant(nm)
         info = vit.describe()
-        print(json.dumps({"profile": prof, "config": a.config or None, "sequences": n, "residues": int(offsets[-1]),
+        print(json.dumps({"profile": prof, "config": a.config or None, "longest_first": a.longest_first,
+                          "sequences": n, "residues": int(offsets[-1]),
                           "variant": nm, "ms_med": round(ms, 4), "ms_min": round(min(res[nm]), 4),
                           "gcups": round(cells / (ms * 1e-3) / 1e9, 1),
                           "valu_frac": round(OPS_PER_CELL * cells / (ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
