@@ -55,18 +55,16 @@ msv_status err_status(uint32_t err) {
     return err ? MSV_ERR_INVALID_ARGUMENT : MSV_OK;
 }
 
-// The cheapest variant covering `states`: fewest slots, then the most transition arrays in VGPRs, then
-// match scores in LDS.  Informative insert scores need an isc variant.
+// The automatic choice covering `states`: among the variants marked `pick` (one per S and insert mode, by
+// measurement), the fewest slots.  Informative insert scores need an isc variant.
 const vitk::VitVariant* pick_variant(uint32_t states, bool isc) {
     int n = 0;
     const vitk::VitVariant* all = vitk::vit_variants(&n);
     const vitk::VitVariant* best = nullptr;
     for (int i = 0; i < n; ++i) {
         const vitk::VitVariant& v = all[i];
-        if (v.isc != isc || static_cast<uint32_t>(v.states()) < states) continue;
-        if (!best || v.S < best->S || (v.S == best->S && (v.ntreg > best->ntreg ||
-                                                          (v.ntreg == best->ntreg && v.elds && !best->elds))))
-            best = &v;
+        if (!v.pick || v.isc != isc || static_cast<uint32_t>(v.states()) < states) continue;
+        if (!best || v.S < best->S) best = &v;
     }
     return best;
 }

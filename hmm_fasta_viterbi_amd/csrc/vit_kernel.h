@@ -39,12 +39,14 @@ struct VitArgs {
 // One compiled instantiation: S states per lane (G = 64 lanes per sequence, covers 64 * S states), the first
 // `ntreg` transition arrays in VGPRs and the rest in LDS, match scores in LDS (elds) or read from L2 every
 // row, informative insert scores (isc, read from L2) or HMMER3's zero insert scores; `waves` 64-lane waves
-// per workgroup.
+// per workgroup.  `pick`: the automatic choice for its S (one per S and insert mode, chosen by measurement,
+// profiles/r04_vit_tune_*.jsonl); the others are A/B candidates reachable through msv_vit_profile_set_variant.
 struct VitVariant {
     int S;
     int ntreg;
     bool elds, isc;
     int waves;
+    bool pick;
     const void* fn;
     const char* name;
     int lds_bytes;

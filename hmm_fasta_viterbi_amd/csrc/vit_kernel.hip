@@ -73,8 +73,8 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
     static_assert(S >= 2 && S % 2 == 0, "S must be even");
     // Rows two per loop trip where the registers allow it (the copies at a one-row loop's back edge); the
     // long rows of the L2 variants (S > 24) keep one row per trip: two rows' register assignments did not
-    // fit 256 VGPRs there (S = 38: 83-124 spilled VGPRs).
-    constexpr bool TWO_ROWS = S <= 24;
+    // fit 256 VGPRs there (S = 38: 83-124 spilled VGPRs), nor 168 at three waves per SIMD (S = 22: 60 -> 16).
+    constexpr bool TWO_ROWS = S <= 24 && WAVES <= 8;
     constexpr int C2 = S / 2;
     constexpr int ROW2 = C2 * kLanes;                     // float2 per table row
     constexpr int NTL = kTransitions - NTREG;             // transition arrays in LDS
@@ -404,74 +404,92 @@ hipError_t launch_select(const float* scores, const uint64_t* offsets, const uin
 // transitions move to LDS and match scores are read from L2 every row.  isc variants (insert_mode 1) read
 // insert scores from L2 and keep transitions in LDS.
 // ------------------------------------------------------------------------------------------------
-#define VIT_VARIANT(S_, NT_, ELDS_, ISC_, W_, PD_, ASC_, NAME_)                                        \
+#define VIT_VARIANT(S_, NT_, ELDS_, ISC_, W_, PD_, ASC_, PICK_, NAME_)                                 \
     VitVariant{S_,                                                                                       \
                NT_,                                                                                      \
                ELDS_,                                                                                    \
                ISC_,                                                                                     \
                W_,                                                                                       \
+               PICK_,                                                                                    \
                reinterpret_cast<const void*>(&vit_kernel<S_, NT_, ELDS_, ISC_, W_, PD_, ASC_>),          \
                NAME_,                                                                                    \
                (ELDS_ ? kRows * (S_)*kLanes * 4 : 0) + (kTransitions - (NT_)) * (S_)*kLanes * 4}
 
+// `P` marks the automatic choice per S (interleaved timings on the MSV survivors of cfg3 / cfg5 and on cfg2,
+// profiles/r04_vit_tune_cfg{2,3,5}.jsonl); `-` are the A/B candidates kept selectable by name.
+#define P true
+#define X false
 const VitVariant* vit_variants(int* count) {
     static const VitVariant all[] = {
         // every transition array in VGPRs, match scores in LDS
-        VIT_VARIANT(2, 7, true, false, 8, 0, false, "vit_s2_t7"),
-        VIT_VARIANT(4, 7, true, false, 8, 0, false, "vit_s4_t7"),
-        VIT_VARIANT(6, 7, true, false, 8, 0, false, "vit_s6_t7"),
-        VIT_VARIANT(8, 7, true, false, 8, 0, false, "vit_s8_t7"),
-        VIT_VARIANT(10, 7, true, false, 8, 0, false, "vit_s10_t7"),
-        VIT_VARIANT(12, 7, true, false, 8, 0, false, "vit_s12_t7"),
-        VIT_VARIANT(14, 7, true, false, 8, 0, false, "vit_s14_t7"),
-        VIT_VARIANT(16, 7, true, false, 8, 0, false, "vit_s16_t7"),
-        VIT_VARIANT(18, 7, true, false, 8, 0, false, "vit_s18_t7"),
+        VIT_VARIANT(2, 7, true, false, 8, 0, false, P, "vit_s2_t7"),
+        VIT_VARIANT(4, 7, true, false, 8, 0, false, P, "vit_s4_t7"),
+        VIT_VARIANT(6, 7, true, false, 8, 0, false, P, "vit_s6_t7"),
+        VIT_VARIANT(8, 7, true, false, 8, 0, false, P, "vit_s8_t7"),
+        VIT_VARIANT(10, 7, true, false, 8, 0, false, P, "vit_s10_t7"),
+        VIT_VARIANT(12, 7, true, false, 8, 0, false, P, "vit_s12_t7"),
+        VIT_VARIANT(14, 7, true, false, 8, 0, false, P, "vit_s14_t7"),
+        VIT_VARIANT(16, 7, true, false, 8, 0, false, P, "vit_s16_t7"),
+        VIT_VARIANT(18, 7, true, false, 8, 0, false, P, "vit_s18_t7"),
         // five arrays in VGPRs, the D chain's two (MD, DD) in LDS
-        VIT_VARIANT(16, 5, true, false, 8, 1, false, "vit_s16_t5"),
-        VIT_VARIANT(18, 5, true, false, 8, 1, false, "vit_s18_t5"),
-        VIT_VARIANT(20, 5, true, false, 8, 1, false, "vit_s20_t5"),
-        VIT_VARIANT(22, 5, true, false, 8, 1, false, "vit_s22_t5"),
-        VIT_VARIANT(24, 5, true, false, 8, 1, false, "vit_s24_t5"),
+        VIT_VARIANT(16, 5, true, false, 8, 1, false, X, "vit_s16_t5"),
+        VIT_VARIANT(18, 5, true, false, 8, 1, false, X, "vit_s18_t5"),
+        VIT_VARIANT(20, 5, true, false, 8, 1, false, X, "vit_s20_t5"),
+        VIT_VARIANT(22, 5, true, false, 8, 1, false, X, "vit_s22_t5"),
+        VIT_VARIANT(24, 5, true, false, 8, 1, false, X, "vit_s24_t5"),
         // every transition array in LDS, match scores in LDS
-        VIT_VARIANT(16, 0, true, false, 8, 1, false, "vit_s16_t0"),
-        VIT_VARIANT(22, 0, true, false, 8, 1, false, "vit_s22_t0"),
+        VIT_VARIANT(16, 0, true, false, 8, 1, false, X, "vit_s16_t0"),
+        VIT_VARIANT(22, 0, true, false, 8, 1, false, X, "vit_s22_t0"),
         // transitions in LDS, match scores from L2
-        VIT_VARIANT(28, 0, false, false, 8, 3, false, "vit_s28_t0g"),
-        VIT_VARIANT(32, 0, false, false, 8, 3, false, "vit_s32_t0g"),
-        VIT_VARIANT(38, 0, false, false, 8, 3, false, "vit_s38_t0g"),
-        VIT_VARIANT(48, 0, false, false, 8, 3, false, "vit_s48_t0g"),
-        VIT_VARIANT(64, 0, false, false, 8, 3, false, "vit_s64_t0g"),
-        // the row as one ascending pass (D chain interleaved with the M/I work): A/B candidates
-        VIT_VARIANT(8, 7, true, false, 8, 0, true, "vit_s8_t7a"),
-        VIT_VARIANT(16, 7, true, false, 8, 0, true, "vit_s16_t7a"),
-        VIT_VARIANT(18, 7, true, false, 8, 0, true, "vit_s18_t7a"),
-        VIT_VARIANT(22, 5, true, false, 8, 1, true, "vit_s22_t5a"),
-        VIT_VARIANT(22, 0, true, false, 8, 1, true, "vit_s22_t0a"),
-        VIT_VARIANT(38, 0, false, false, 8, 3, true, "vit_s38_t0ga"),
+        VIT_VARIANT(24, 0, false, false, 8, 3, false, X, "vit_s24_t0g"),
+        VIT_VARIANT(26, 0, false, false, 8, 3, false, X, "vit_s26_t0g"),
+        VIT_VARIANT(28, 0, false, false, 8, 3, false, P, "vit_s28_t0g"),
+        VIT_VARIANT(30, 0, false, false, 8, 3, false, P, "vit_s30_t0g"),
+        VIT_VARIANT(32, 0, false, false, 8, 3, false, P, "vit_s32_t0g"),
+        VIT_VARIANT(38, 0, false, false, 8, 3, false, X, "vit_s38_t0g"),
+        VIT_VARIANT(48, 0, false, false, 8, 3, false, X, "vit_s48_t0g"),
+        VIT_VARIANT(64, 0, false, false, 8, 3, false, P, "vit_s64_t0g"),
+        // the row as one ascending pass (D chain interleaved with the M/I work): cfg3 1.68 vs 1.85 ms at S = 22
+        VIT_VARIANT(8, 7, true, false, 8, 0, true, X, "vit_s8_t7a"),
+        VIT_VARIANT(16, 7, true, false, 8, 0, true, X, "vit_s16_t7a"),
+        VIT_VARIANT(18, 7, true, false, 8, 0, true, X, "vit_s18_t7a"),
+        VIT_VARIANT(20, 5, true, false, 8, 1, true, P, "vit_s20_t5a"),
+        VIT_VARIANT(22, 5, true, false, 8, 1, true, P, "vit_s22_t5a"),
+        VIT_VARIANT(22, 0, true, false, 8, 1, true, X, "vit_s22_t0a"),
+        VIT_VARIANT(38, 0, false, false, 8, 3, true, X, "vit_s38_t0ga"),
         // one wave per SIMD (4 per workgroup): the 512-register budget holds S = 38 without the 52 spilled
-        // VGPRs of the 8-wave form (S = 48: 12 instead of 169): A/B candidates
-        VIT_VARIANT(38, 0, false, false, 4, 1, false, "vit_s38_t0g4"),
-        VIT_VARIANT(48, 0, false, false, 4, 3, false, "vit_s48_t0g4"),
-        // one wave per SIMD with every transition array in registers (no transition reads from LDS)
-        VIT_VARIANT(16, 7, true, false, 4, 0, false, "vit_s16_t7w4"),
-        VIT_VARIANT(22, 7, true, false, 4, 0, false, "vit_s22_t7w4"),
-        VIT_VARIANT(22, 7, true, false, 4, 0, true, "vit_s22_t7w4a"),
-        VIT_VARIANT(24, 7, true, false, 4, 0, false, "vit_s24_t7w4"),
-        VIT_VARIANT(28, 7, true, false, 4, 0, false, "vit_s28_t7w4"),
-        VIT_VARIANT(38, 7, false, false, 4, 3, false, "vit_s38_t7gw4"),
-        VIT_VARIANT(48, 7, false, false, 4, 3, false, "vit_s48_t7gw4"),
+        // VGPRs of the 8-wave form (S = 48: 12 instead of 169)
+        VIT_VARIANT(38, 0, false, false, 4, 1, false, X, "vit_s38_t0g4"),
+        VIT_VARIANT(48, 0, false, false, 4, 3, false, P, "vit_s48_t0g4"),
+        // one wave per SIMD with every transition array in registers (no transition reads from LDS): slower
+        // than two waves per SIMD where those fit (S = 22), faster where they spill (S = 24, 38)
+        VIT_VARIANT(16, 7, true, false, 4, 0, false, X, "vit_s16_t7w4"),
+        VIT_VARIANT(22, 7, true, false, 4, 0, false, X, "vit_s22_t7w4"),
+        VIT_VARIANT(22, 7, true, false, 4, 0, true, X, "vit_s22_t7w4a"),
+        VIT_VARIANT(24, 7, true, false, 4, 0, false, P, "vit_s24_t7w4"),
+        VIT_VARIANT(26, 7, true, false, 4, 0, false, X, "vit_s26_t7w4"),
+        VIT_VARIANT(28, 7, true, false, 4, 0, false, X, "vit_s28_t7w4"),
+        VIT_VARIANT(34, 7, false, false, 4, 3, false, P, "vit_s34_t7gw4"),
+        VIT_VARIANT(36, 7, false, false, 4, 3, false, P, "vit_s36_t7gw4"),
+        VIT_VARIANT(38, 7, false, false, 4, 3, false, P, "vit_s38_t7gw4"),
+        VIT_VARIANT(48, 7, false, false, 4, 3, false, X, "vit_s48_t7gw4"),
+        // three waves per SIMD (12 per workgroup, <= 168 VGPRs; 16 / 40 spilled): transitions in LDS
+        VIT_VARIANT(22, 0, true, false, 12, 1, true, X, "vit_s22_t0w12a"),
+        VIT_VARIANT(22, 0, true, false, 12, 1, false, X, "vit_s22_t0w12"),
         // informative insert scores (insert_mode 1): transitions in LDS, match and insert scores from L2
-        VIT_VARIANT(2, 0, false, true, 8, 3, false, "vit_s2_t0gi"),
-        VIT_VARIANT(8, 0, false, true, 8, 3, false, "vit_s8_t0gi"),
-        VIT_VARIANT(16, 0, false, true, 8, 3, false, "vit_s16_t0gi"),
-        VIT_VARIANT(22, 0, false, true, 8, 3, false, "vit_s22_t0gi"),
-        VIT_VARIANT(32, 0, false, true, 8, 3, false, "vit_s32_t0gi"),
-        VIT_VARIANT(38, 0, false, true, 8, 3, false, "vit_s38_t0gi"),
-        VIT_VARIANT(64, 0, false, true, 8, 3, false, "vit_s64_t0gi"),
+        VIT_VARIANT(2, 0, false, true, 8, 3, false, P, "vit_s2_t0gi"),
+        VIT_VARIANT(8, 0, false, true, 8, 3, false, P, "vit_s8_t0gi"),
+        VIT_VARIANT(16, 0, false, true, 8, 3, false, P, "vit_s16_t0gi"),
+        VIT_VARIANT(22, 0, false, true, 8, 3, false, P, "vit_s22_t0gi"),
+        VIT_VARIANT(32, 0, false, true, 8, 3, false, P, "vit_s32_t0gi"),
+        VIT_VARIANT(38, 0, false, true, 8, 3, false, P, "vit_s38_t0gi"),
+        VIT_VARIANT(64, 0, false, true, 8, 3, false, P, "vit_s64_t0gi"),
     };
     *count = static_cast<int>(sizeof(all) / sizeof(all[0]));
     return all;
 }
+#undef P
+#undef X
 
 hipError_t vit_launch(const VitVariant& v, uint32_t blocks, const VitArgs& args, hipStream_t stream, hipEvent_t start,
                       hipEvent_t stop) {
