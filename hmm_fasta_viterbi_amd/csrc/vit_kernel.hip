@@ -73,8 +73,8 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
     static_assert(S >= 2 && S % 2 == 0, "S must be even");
     // Rows two per loop trip where the registers allow it (the copies at a one-row loop's back edge); the
     // long rows of the L2 variants (S > 24) keep one row per trip: two rows' register assignments did not
-    // fit 256 VGPRs there (S = 38: 83-124 spilled VGPRs), nor 168 at three waves per SIMD (S = 22: 60 -> 16).
-    constexpr bool TWO_ROWS = S <= 24 && WAVES <= 8;
+    // fit 256 VGPRs there (S = 38: 83-124 spilled VGPRs).
+    constexpr bool TWO_ROWS = S <= 24;
     constexpr int C2 = S / 2;
     constexpr int ROW2 = C2 * kLanes;                     // float2 per table row
     constexpr int NTL = kTransitions - NTREG;             // transition arrays in LDS
@@ -441,8 +441,8 @@ const VitVariant* vit_variants(int* count) {
         VIT_VARIANT(16, 0, true, false, 8, 1, false, X, "vit_s16_t0"),
         VIT_VARIANT(22, 0, true, false, 8, 1, false, X, "vit_s22_t0"),
         // transitions in LDS, match scores from L2
-        VIT_VARIANT(24, 0, false, false, 8, 3, false, X, "vit_s24_t0g"),
-        VIT_VARIANT(26, 0, false, false, 8, 3, false, X, "vit_s26_t0g"),
+        VIT_VARIANT(24, 0, false, false, 8, 3, false, P, "vit_s24_t0g"),
+        VIT_VARIANT(26, 0, false, false, 8, 3, false, P, "vit_s26_t0g"),
         VIT_VARIANT(28, 0, false, false, 8, 3, false, P, "vit_s28_t0g"),
         VIT_VARIANT(30, 0, false, false, 8, 3, false, P, "vit_s30_t0g"),
         VIT_VARIANT(32, 0, false, false, 8, 3, false, P, "vit_s32_t0g"),
@@ -462,20 +462,17 @@ const VitVariant* vit_variants(int* count) {
         VIT_VARIANT(38, 0, false, false, 4, 1, false, X, "vit_s38_t0g4"),
         VIT_VARIANT(48, 0, false, false, 4, 3, false, P, "vit_s48_t0g4"),
         // one wave per SIMD with every transition array in registers (no transition reads from LDS): slower
-        // than two waves per SIMD where those fit (S = 22), faster where they spill (S = 24, 38)
+        // than two waves per SIMD where those fit without spilling (S = 22-32), faster where they spill (34-38)
         VIT_VARIANT(16, 7, true, false, 4, 0, false, X, "vit_s16_t7w4"),
         VIT_VARIANT(22, 7, true, false, 4, 0, false, X, "vit_s22_t7w4"),
         VIT_VARIANT(22, 7, true, false, 4, 0, true, X, "vit_s22_t7w4a"),
-        VIT_VARIANT(24, 7, true, false, 4, 0, false, P, "vit_s24_t7w4"),
+        VIT_VARIANT(24, 7, true, false, 4, 0, false, X, "vit_s24_t7w4"),
         VIT_VARIANT(26, 7, true, false, 4, 0, false, X, "vit_s26_t7w4"),
         VIT_VARIANT(28, 7, true, false, 4, 0, false, X, "vit_s28_t7w4"),
         VIT_VARIANT(34, 7, false, false, 4, 3, false, P, "vit_s34_t7gw4"),
         VIT_VARIANT(36, 7, false, false, 4, 3, false, P, "vit_s36_t7gw4"),
         VIT_VARIANT(38, 7, false, false, 4, 3, false, P, "vit_s38_t7gw4"),
         VIT_VARIANT(48, 7, false, false, 4, 3, false, X, "vit_s48_t7gw4"),
-        // three waves per SIMD (12 per workgroup, <= 168 VGPRs; 16 / 40 spilled): transitions in LDS
-        VIT_VARIANT(22, 0, true, false, 12, 1, true, X, "vit_s22_t0w12a"),
-        VIT_VARIANT(22, 0, true, false, 12, 1, false, X, "vit_s22_t0w12"),
         // informative insert scores (insert_mode 1): transitions in LDS, match and insert scores from L2
         VIT_VARIANT(2, 0, false, true, 8, 3, false, P, "vit_s2_t0gi"),
         VIT_VARIANT(8, 0, false, true, 8, 3, false, P, "vit_s8_t0gi"),
