@@ -303,6 +303,47 @@ def viterbi_stage(args, msv_engine, prof_path, dev, stream, d_res, residues, d_o
     }
 
 
+def latency_ceiling(engine, dev, sh, n, lmax, longest, kernel_ms, hip_event, hip_elapsed_ms) -> dict:
+    """cfg2's measured floor (tools/cfg2_floor.py is the standalone form): a batch that
+    fits the grid once ends when its longest sequence's rows end, so the floor is those rows at the fastest
+    row time the plan has -- one wave per SIMD (n = 4096 uniform-length sequences: 1,024 waves of the 16-lane
+    plan's 4 sequences each) -- and the same batch size with every sequence at the longest length bounds it
+    from above at this occupancy.  Both timed here, on this box, with the launches' own HIP events."""
+    import torch
+
+    from hmm_fasta_viterbi_amd.synthetic import random_batch
+
+    def timed(codes, offsets, reps=15):
+        m = len(offsets) - 1
+        r = torch.from_numpy(codes).to(dev)
+        o = torch.from_numpy(offsets.view(np.int64)).to(dev)
+        s = torch.empty(m, dtype=torch.float32, device=dev)
+        od = torch.empty(m, dtype=torch.int32, device=dev)
+        evs = []
+        for k in range(reps + 3):
+            engine.order_longest_first(o.data_ptr(), m, od.data_ptr(), sh)
+            ev = (hip_event(), hip_event()) if k >= 3 else None
+            if ev:
+                _native.lib().msv_debug_time_next_launch(engine._p, ev[0], ev[1])
+                evs.append(ev)
+            engine.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), m, s.data_ptr(), od.data_ptr(), sh)
+        engine.check(sh)
+        torch.cuda.synchronize(dev)
+        return float(np.median([hip_elapsed_ms(a, b) for a, b in evs])), engine.variant_for(m)
+
+    from hmm_fasta_viterbi_amd import _native
+    one_ms, one_var = timed(*random_batch(77, 4096, lmax, lmax))
+    row_ns = one_ms * 1e6 / lmax
+    uni_ms, _ = timed(*random_batch(90, n, lmax, lmax))
+    floor_ms = longest * row_ns / 1e6
+    return {"row_ns_one_wave_per_simd": round(row_ns, 2), "one_wave_variant": one_var, "longest_rows": int(longest),
+            "floor_ms": round(floor_ms, 4), "kernel_over_floor": round(kernel_ms / floor_ms, 4),
+            "uniform_longest_ms": round(uni_ms, 4), "kernel_over_uniform_longest": round(kernel_ms / uni_ms, 4),
+            "note": "floor = the batch's longest sequence at the one-wave-per-SIMD row time (4,096 sequences of "
+                    "the longest length, 1,024 waves); uniform_longest = this batch size with every sequence "
+                    "that long (the occupancy this batch runs at, no shorter co-resident waves)"}
+
+
 def per_rank_summary(allr, steps: int, scaling: str) -> dict:
     """Each rank's own figures for an N-rank line: allr = [world, 4] rows of {elapsed s,
     kernel ms, residues, sequences} as all-gathered after the timed window; min / max / max-over-min of the
@@ -773,6 +814,10 @@ def main(args=None):
             },
             "scores_finite_and_consistent": ok,
         }
+        if args.config == "cfg2":  # the latency-bound config: its measured floor beside the kernel
+            result["latency_ceiling"] = latency_ceiling(engine, dev, sh, n, lmax,
+                                                        int(np.diff(offsets.astype(np.int64)).max()), kernel_ms,
+                                                        hip_event, hip_elapsed_ms)
         if not args.no_viterbi:
             result["viterbi_stage"] = viterbi_stage(args, engine, prof_path, dev, stream, d_res, residues, d_off, n,
                                                     d_scores, None if args.no_order else d_order, codes, offsets,

@@ -69,7 +69,9 @@ def device_scores(engine, codes, offsets, order=True):
 
 
 @pytest.mark.timeout(900)
-def test_cfg4_full_size_three_ways():
+def test_cfg4_full_size_every_score():
+    """cfg4 (1400.hmm x 1M, one set): one launch, the host pipeline, 8 shards through msv_score_batch_multi and
+    the torch.distributed slices all bitwise equal, and every score equal to the oracle's."""
     prof = msv.Profile_HMM(profile_path("1400.hmm"))
     e = msv.MSV_HMM(prof)
     codes, offsets = random_batch(3, 1_000_000, 300, 500)
