@@ -68,15 +68,8 @@ struct ChunkD {
 // (bounds the live loads: left alone, the scheduler hoists a whole row of loads and spills).
 // ASC: the row as ONE ascending pass (D chain interleaved with the M/I work) instead of a descending M/I pass
 // followed by an ascending D pass.
-// OPT bit 0 (MB): one wave-level branch per row -- the lazy-F test and the J >= N test share one ballot, the
-//   rare path then tells them apart (J does not depend on D, so it is made before the D chain is final).
-// OPT bit 1 (XP, ASC only): the next row's first LDS/L2 chunks (the peeled last chunk and PD chunks from the
-//   front) are requested at the end of this row, before its wave-level branches, so a row does not start
-//   with a load latency.
-template <int S, int NTREG, bool ELDS, bool ISC, int WAVES, int PD, bool ASC, int OPT = 0>
+template <int S, int NTREG, bool ELDS, bool ISC, int WAVES, int PD, bool ASC>
 __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
-    constexpr bool MB = (OPT & 1) != 0;
-    constexpr bool XP = ASC && PD > 0 && (OPT & 2) != 0;
     static_assert(S >= 2 && S % 2 == 0, "S must be even");
     // Rows two per loop trip where the registers allow it (the copies at a one-row loop's back edge); the
     // long rows of the L2 variants (S > 24) keep one row per trip: two rows' register assignments did not
@@ -150,48 +143,6 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
             const uint8_t* res = a.residues + o0;
             uint32_t cur = static_cast<uint64_t>(lane) < L ? res[lane] : 0u;
             uint32_t nxt = static_cast<uint64_t>(64 + lane) < L ? res[64 + lane] : 0u;
-            // row tables of residue code `code` (clamped to 19; codes >= 20 are flagged through maxcode)
-            auto er_of = [&](uint32_t code) -> const float2* {
-                if constexpr (ELDS) return etab_s + code * ROW2 + lane;  // (one address space per variant)
-                else return a.etab + code * ROW2 + lane;
-            };
-            auto load_mi_at = [&](const float2* er, const float2* ir, int c) {
-                ChunkMI<NM> k;
-#pragma unroll
-                for (int j = 0; j < NM; ++j) k.t[j] = tlds(NTREG + j, c);
-                k.e = er[c * kLanes];
-                if constexpr (ISC) k.i = ir[c * kLanes];
-                return k;
-            };
-            auto load_d_at = [&](int c) {
-                ChunkD<ND> k;
-#pragma unroll
-                for (int j = 0; j < ND; ++j) k.t[j] = tlds(kTransitions - ND + j, c);
-                return k;
-            };
-            // XP: the first chunks of the next row, requested at the end of the current one
-            struct Pref {
-                ChunkMI<NM> kl;
-                ChunkMI<NM> km[XP ? (PD < C2 - 1 ? PD : C2 - 1) : 1];
-                ChunkD<ND> kd[XP ? (PD < C2 ? PD : C2) : 1];
-            } pf;
-            auto prefetch = [&](uint32_t code) {
-                if constexpr (XP) {
-                    const float2* er = er_of(code);
-                    const float2* ir = a.itab + code * ROW2 + lane;
-                    pf.kl = load_mi_at(er, ir, C2 - 1);
-#pragma unroll
-                    for (int c = 0; c < PD && c < C2 - 1; ++c) pf.km[c] = load_mi_at(er, ir, c);
-                    if constexpr (ND > 0) {
-#pragma unroll
-                        for (int c = 0; c < PD && c < C2; ++c) pf.kd[c] = load_d_at(c);
-                    }
-                }
-            };
-            if constexpr (XP) {
-                const uint32_t c0 = __builtin_amdgcn_readlane(cur, 0);
-                prefetch(c0 < 19u ? c0 : 19u);
-            }
             // One row (residue i).  Rows run two per loop trip: a row writes its new M into registers other
             // than the old ones (the old M(k) is read after the new one is made), so a one-row loop copied
             // the whole row back at its back edge (22 v_mov per row at S = 22); over two rows the values
@@ -207,10 +158,24 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                 code = code < 19u ? code : 19u;
                 if constexpr (NTL > 0) asm volatile("" : "+v"(rz));
                 const float Bt = B + a.tr_B_Mk;
-                const float2* er = er_of(code);
+                const float2* er;
+                if constexpr (ELDS) er = etab_s + code * ROW2 + lane;  // (one address space per variant)
+                else er = a.etab + code * ROW2 + lane;
                 const float2* ir = a.itab + code * ROW2 + lane;
-                auto load_mi = [&](int c) { return load_mi_at(er, ir, c); };
-                auto load_d = [&](int c) { return load_d_at(c); };
+                auto load_mi = [&](int c) {
+                    ChunkMI<NM> k;
+#pragma unroll
+                    for (int j = 0; j < NM; ++j) k.t[j] = tlds(NTREG + j, c);
+                    k.e = er[c * kLanes];
+                    if constexpr (ISC) k.i = ir[c * kLanes];
+                    return k;
+                };
+                auto load_d = [&](int c) {
+                    ChunkD<ND> k;
+#pragma unroll
+                    for (int j = 0; j < ND; ++j) k.t[j] = tlds(kTransitions - ND + j, c);
+                    return k;
+                };
                 auto Tm = [&](const ChunkMI<NM>& k, int j, int q) -> float {  // j in MM_IN .. II
                     if (j < NTREG) return tr[j < NTREG ? j : 0][q];
                     const float2 t = k.t[j >= NTREG ? j - NTREG : 0];
@@ -233,20 +198,14 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                     // in three registers) and its D the new M(q-1) and D(q-1), so the D chain runs interleaved
                     // with the independent M/I work.  The lane's last M is made first (peeled) so it can cross
                     // to the next lane for that lane's first D.
-                    const ChunkMI<NM> kl = XP ? pf.kl : load_mi(C2 - 1);
+                    const ChunkMI<NM> kl = load_mi(C2 - 1);
                     const float mlast = fmaxf(fmaxf(M[S - 2] + Tm(kl, MM_IN, S - 1), I[S - 2] + Tm(kl, IM_IN, S - 1)),
                                               fmaxf(D[S - 2] + Tm(kl, DM_IN, S - 1), Bt)) +
                                         kl.e.y;
                     sMn = shift64(mlast, sMn);
                     ChunkMI<NM> km[C2];
                     ChunkD<ND> kd[C2];
-                    if constexpr (XP) {
-#pragma unroll
-                        for (int c = 0; c < C2 && c < PD; ++c) {
-                            if (c < C2 - 1) km[c] = pf.km[c];
-                            if constexpr (ND > 0) kd[c] = pf.kd[c];
-                        }
-                    } else if constexpr (PD > 0) {
+                    if constexpr (PD > 0) {
 #pragma unroll
                         for (int c = 0; c < C2 && c < PD; ++c) {
                             if (c < C2 - 1) km[c] = load_mi(c);
@@ -348,15 +307,10 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                         if constexpr (PD > 0 && ND > 0) __builtin_amdgcn_sched_barrier(0);
                     }
                 }
-                if constexpr (XP) {  // the next row's first chunks, before this row's wave-level branches
-                    const uint32_t ph1 = (ph + 1u) & 63u;
-                    uint32_t cn = __builtin_amdgcn_readlane(ph1 == 0 ? nxt : cur, ph1);
-                    prefetch(cn < 19u ? cn : 19u);
-                }
                 // lazy-F: carry D across lane boundaries until no lane's first state changes
                 sDn = shift64(D[S - 1], sDn);
                 float cand = sDn + tdd(0);
-                auto lazy_f = [&]() {
+                if (__builtin_expect(wave_any(cand > D[0]), 0)) {
                     do {
                         D[0] = fmaxf(D[0], cand);
 #pragma unroll
@@ -364,24 +318,13 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                         sDn = shift64(D[S - 1], sDn);
                         cand = sDn + tdd(0);
                     } while (wave_any(cand > D[0]));
-                };
-                if constexpr (!MB) {
-                    if (__builtin_expect(wave_any(cand > D[0]), 0)) lazy_f();
                 }
                 // specials (MSV_HMM.cpp:107-110), J and C as per-lane partials
                 J = fmaxf(J + loop, E + a.tr_E_J);
                 Cp = fmaxf(Cp + loop, E + a.tr_E_C);
                 N = N + loop;
                 B = N + move;
-                if constexpr (MB) {
-                    const bool fix = cand > D[0];
-                    if (__builtin_expect(wave_any(fix || J >= N), 0)) {
-                        if (wave_any(fix)) lazy_f();
-                        if (wave_any(J >= N)) B = fmaxf(N, msvk::group_max<64>(J)) + move;
-                    }
-                } else {
-                    if (wave_any(J >= N)) B = fmaxf(N, msvk::group_max<64>(J)) + move;
-                }
+                if (wave_any(J >= N)) B = fmaxf(N, msvk::group_max<64>(J)) + move;
             };
             uint64_t i = 0;
             if constexpr (TWO_ROWS) {
@@ -461,18 +404,16 @@ hipError_t launch_select(const float* scores, const uint64_t* offsets, const uin
 // transitions move to LDS and match scores are read from L2 every row.  isc variants (insert_mode 1) read
 // insert scores from L2 and keep transitions in LDS.
 // ------------------------------------------------------------------------------------------------
-#define VIT_VARIANT_O(S_, NT_, ELDS_, ISC_, W_, PD_, ASC_, OPT_, PICK_, NAME_)                         \
+#define VIT_VARIANT(S_, NT_, ELDS_, ISC_, W_, PD_, ASC_, PICK_, NAME_)                                 \
     VitVariant{S_,                                                                                       \
                NT_,                                                                                      \
                ELDS_,                                                                                    \
                ISC_,                                                                                     \
                W_,                                                                                       \
                PICK_,                                                                                    \
-               reinterpret_cast<const void*>(&vit_kernel<S_, NT_, ELDS_, ISC_, W_, PD_, ASC_, OPT_>),    \
+               reinterpret_cast<const void*>(&vit_kernel<S_, NT_, ELDS_, ISC_, W_, PD_, ASC_>),          \
                NAME_,                                                                                    \
                (ELDS_ ? kRows * (S_)*kLanes * 4 : 0) + (kTransitions - (NT_)) * (S_)*kLanes * 4}
-#define VIT_VARIANT(S_, NT_, ELDS_, ISC_, W_, PD_, ASC_, PICK_, NAME_) \
-    VIT_VARIANT_O(S_, NT_, ELDS_, ISC_, W_, PD_, ASC_, 0, PICK_, NAME_)
 
 // `P` marks the automatic choice per S (interleaved timings on the MSV survivors of cfg3 / cfg5 and on cfg2,
 // profiles/r04_vit_tune_cfg{2,3,5}.jsonl); `-` are the A/B candidates kept selectable by name.
@@ -515,13 +456,6 @@ const VitVariant* vit_variants(int* count) {
         VIT_VARIANT(20, 5, true, false, 8, 1, true, P, "vit_s20_t5a"),
         VIT_VARIANT(22, 5, true, false, 8, 1, true, P, "vit_s22_t5a"),
         VIT_VARIANT(22, 0, true, false, 8, 1, true, X, "vit_s22_t0a"),
-        // one branch per row (m), the next row's first chunks requested early (x), four arrays in VGPRs (t4)
-        VIT_VARIANT_O(22, 5, true, false, 8, 1, true, 1, X, "vit_s22_t5am"),
-        VIT_VARIANT_O(22, 5, true, false, 8, 1, true, 3, X, "vit_s22_t5amx"),
-        VIT_VARIANT_O(22, 4, true, false, 8, 1, true, 1, X, "vit_s22_t4am"),
-        VIT_VARIANT_O(22, 4, true, false, 8, 1, true, 3, X, "vit_s22_t4amx"),
-        VIT_VARIANT_O(22, 4, true, false, 8, 2, true, 3, X, "vit_s22_t4amx2"),
-        VIT_VARIANT_O(22, 5, true, false, 8, 1, false, 1, X, "vit_s22_t5m"),
         VIT_VARIANT(38, 0, false, false, 8, 3, true, X, "vit_s38_t0ga"),
         // one wave per SIMD (4 per workgroup): the 512-register budget holds S = 38 without the 52 spilled
         // VGPRs of the 8-wave form (S = 48: 12 instead of 169)
