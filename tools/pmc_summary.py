@@ -22,12 +22,13 @@ from collections import defaultdict
 
 def main():
     out, cfg = sys.argv[1], sys.argv[2]
+    kname = sys.argv[3] if len(sys.argv) > 3 else "msv_batch_kernel"  # e.g. vit_kernel (tools/run_vit.py)
     vals = defaultdict(list)
     names = set()
     for path in glob.glob(os.path.join(out, "pmc*", "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if "msv_batch_kernel" not in row.get("Kernel_Name", ""):
+                if kname not in row.get("Kernel_Name", ""):
                     continue
                 names.add(row["Kernel_Name"])
                 # per pass: Dispatch_Id restarts in every rocprofv3 run
@@ -35,7 +36,7 @@ def main():
     # Every pass must have measured ONE kernel (tools/run_kernel.py launches the resident variant only);
     # bench.py publishes roofline.traffic only when this name is the kernel its timed steps run.
     if len(names) != 1:
-        sys.exit(f"pmc_summary: expected one msv_batch_kernel instantiation, found {sorted(names)}")
+        sys.exit(f"pmc_summary: expected one {kname} instantiation, found {sorted(names)}")
     per = defaultdict(list)
     for (name, _path, _disp), v in vals.items():
         per[name].append(sum(v))
