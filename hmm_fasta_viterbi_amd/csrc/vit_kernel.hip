@@ -43,6 +43,7 @@ namespace vitk {
 namespace {
 
 constexpr float NINF = -__builtin_inff();
+constexpr int kEarlyD = 8;  // slots of the unconditional first lazy-F pass before its early-exit test
 
 __device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 
@@ -310,7 +311,7 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                 // lazy-F: carry D across lane boundaries until no lane's first state changes
                 sDn = shift64(D[S - 1], sDn);
                 float cand = sDn + tdd(0);
-                if (__builtin_expect(wave_any(cand > D[0]), 0)) {
+                auto lazy_f = [&]() {
                     do {
                         D[0] = fmaxf(D[0], cand);
 #pragma unroll
@@ -318,6 +319,27 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                         sDn = shift64(D[S - 1], sDn);
                         cand = sDn + tdd(0);
                     } while (wave_any(cand > D[0]));
+                };
+                if constexpr (S > kEarlyD) {
+                    // With 64 lanes some D path crosses a lane boundary on nearly every row (1.00 correction
+                    // passes per row on 1400.hmm), and it dies out within a few states (the last state a pass
+                    // changes: median 6, 74% <= 7; tools/lazy_f_stats.py).  So the first pass runs
+                    // unconditionally over slots 0 .. kEarlyD-1, and the rest of the lane only if some lane
+                    // would still change at slot kEarlyD: a slot that changes nowhere stops the chain (every
+                    // later D was computed from the same values), and then no lane's last D changed either,
+                    // so no second pass is needed.  Same max/add sequence per state as the serial chain.
+                    D[0] = fmaxf(D[0], cand);
+#pragma unroll
+                    for (int q = 1; q < kEarlyD; ++q) D[q] = fmaxf(D[q], D[q - 1] + tdd(q));
+                    if (wave_any(D[kEarlyD - 1] + tdd(kEarlyD) > D[kEarlyD])) {
+#pragma unroll
+                        for (int q = kEarlyD; q < S; ++q) D[q] = fmaxf(D[q], D[q - 1] + tdd(q));
+                        sDn = shift64(D[S - 1], sDn);
+                        cand = sDn + tdd(0);
+                        if (wave_any(cand > D[0])) lazy_f();
+                    }
+                } else {
+                    if (__builtin_expect(wave_any(cand > D[0]), 0)) lazy_f();
                 }
                 // specials (MSV_HMM.cpp:107-110), J and C as per-lane partials
                 J = fmaxf(J + loop, E + a.tr_E_J);
