@@ -478,6 +478,9 @@ const VitVariant* vit_variants(int* count) {
         VIT_VARIANT(20, 5, true, false, 8, 1, true, P, "vit_s20_t5a"),
         VIT_VARIANT(22, 5, true, false, 8, 1, true, P, "vit_s22_t5a"),
         VIT_VARIANT(22, 0, true, false, 8, 1, true, X, "vit_s22_t0a"),
+        // LDS chunks requested two ahead (A/B candidates)
+        VIT_VARIANT(22, 5, true, false, 8, 2, true, X, "vit_s22_t5a2"),
+        VIT_VARIANT(22, 5, true, false, 8, 2, false, X, "vit_s22_t5p2"),
         VIT_VARIANT(38, 0, false, false, 8, 3, true, X, "vit_s38_t0ga"),
         // one wave per SIMD (4 per workgroup): the 512-register budget holds S = 38 without the 52 spilled
         // VGPRs of the 8-wave form (S = 48: 12 instead of 169)
@@ -494,6 +497,9 @@ const VitVariant* vit_variants(int* count) {
         VIT_VARIANT(34, 7, false, false, 4, 3, false, P, "vit_s34_t7gw4"),
         VIT_VARIANT(36, 7, false, false, 4, 3, false, P, "vit_s36_t7gw4"),
         VIT_VARIANT(38, 7, false, false, 4, 3, false, P, "vit_s38_t7gw4"),
+        VIT_VARIANT(38, 7, false, false, 4, 2, false, X, "vit_s38_t7gw4p2"),
+        VIT_VARIANT(38, 7, false, false, 4, 4, false, X, "vit_s38_t7gw4p4"),
+        VIT_VARIANT(38, 7, false, false, 4, 3, true, X, "vit_s38_t7gw4a"),
         VIT_VARIANT(48, 7, false, false, 4, 3, false, X, "vit_s48_t7gw4"),
         // informative insert scores (insert_mode 1): transitions in LDS, match and insert scores from L2
         VIT_VARIANT(2, 0, false, true, 8, 3, false, P, "vit_s2_t0gi"),
