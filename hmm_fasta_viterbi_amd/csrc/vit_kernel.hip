@@ -25,8 +25,8 @@
 //     from -inf, then while any lane's incoming D(k-1)+tDD beats its first D, the lanes re-run
 //     D_q = max(D_q, D_{q-1}+tDD).  Lower bounds only ever rise to the exact value and fl() is
 //     monotone, so the result is the serial chain bit for bit;
-//   * J and C are per-lane partials (as the MSV kernel), the 64-lane max taken only when some J >= N
-//     and once per sequence for C;
+//   * J is kept exact and wave-uniform, the 64-lane max of E taken only on rows where some lane's E + tEJ
+//     beats J + loop; C is a per-lane partial, its 64-lane max taken once per sequence;
 //   * match scores staged in LDS ([20][S/2][64] float2: each ds_read_b64 of a wave is contiguous) and the
 //     7 transition arrays in VGPRs, or (large models) transitions in LDS and match scores from L2;
 //   * persistent grid, first sequence static, then one atomic per sequence; the counter resets itself.
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
             float M[S], I[S], D[S];
 #pragma unroll
             for (int q = 0; q < S; ++q) M[q] = I[q] = D[q] = NINF;
-            float J = NINF, Cp = NINF;  // per-lane partials of J and C
+            float J = NINF, Cp = NINF;  // J exact (wave-uniform), C as per-lane partials
             float N = 0.0f, B = move;
             float sM = NINF, sI = NINF, sD = NINF, sMn = NINF, sDn = NINF;  // shift registers, lane 0 = -inf
             uint32_t maxcode = 0;
@@ -341,12 +341,17 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                 } else {
                     if (__builtin_expect(wave_any(cand > D[0]), 0)) lazy_f();
                 }
-                // specials (MSV_HMM.cpp:107-110), J and C as per-lane partials
-                J = fmaxf(J + loop, E + a.tr_E_J);
+                // specials (MSV_HMM.cpp:107-110).  J = max(J + loop, max_k E + tEJ) is kept exact and
+                // wave-uniform: the 64-lane max of E is taken only on rows where some lane's E + tEJ beats
+                // J + loop (a new best segment forming; fl() is monotone, so max_l fl(E_l + t) = fl(max_l E_l
+                // + t)).  Per-lane J partials (the MSV kernel's form) needed the 64-lane max of J on every row
+                // after the first hit, and the filter's survivors are the sequences with hits.
+                const float Jn = J + loop;
+                J = __builtin_expect(wave_any(E + a.tr_E_J > Jn), 0) ? fmaxf(Jn, msvk::group_max<64>(E) + a.tr_E_J)
+                                                                       : Jn;
                 Cp = fmaxf(Cp + loop, E + a.tr_E_C);
                 N = N + loop;
-                B = N + move;
-                if (wave_any(J >= N)) B = fmaxf(N, msvk::group_max<64>(J)) + move;
+                B = fmaxf(N, J) + move;
             };
             uint64_t i = 0;
             if constexpr (TWO_ROWS) {
@@ -478,9 +483,6 @@ const VitVariant* vit_variants(int* count) {
         VIT_VARIANT(20, 5, true, false, 8, 1, true, P, "vit_s20_t5a"),
         VIT_VARIANT(22, 5, true, false, 8, 1, true, P, "vit_s22_t5a"),
         VIT_VARIANT(22, 0, true, false, 8, 1, true, X, "vit_s22_t0a"),
-        // LDS chunks requested two ahead (A/B candidates)
-        VIT_VARIANT(22, 5, true, false, 8, 2, true, X, "vit_s22_t5a2"),
-        VIT_VARIANT(22, 5, true, false, 8, 2, false, X, "vit_s22_t5p2"),
         VIT_VARIANT(38, 0, false, false, 8, 3, true, X, "vit_s38_t0ga"),
         // one wave per SIMD (4 per workgroup): the 512-register budget holds S = 38 without the 52 spilled
         // VGPRs of the 8-wave form (S = 48: 12 instead of 169)
@@ -497,9 +499,6 @@ const VitVariant* vit_variants(int* count) {
         VIT_VARIANT(34, 7, false, false, 4, 3, false, P, "vit_s34_t7gw4"),
         VIT_VARIANT(36, 7, false, false, 4, 3, false, P, "vit_s36_t7gw4"),
         VIT_VARIANT(38, 7, false, false, 4, 3, false, P, "vit_s38_t7gw4"),
-        VIT_VARIANT(38, 7, false, false, 4, 2, false, X, "vit_s38_t7gw4p2"),
-        VIT_VARIANT(38, 7, false, false, 4, 4, false, X, "vit_s38_t7gw4p4"),
-        VIT_VARIANT(38, 7, false, false, 4, 3, true, X, "vit_s38_t7gw4a"),
         VIT_VARIANT(48, 7, false, false, 4, 3, false, X, "vit_s48_t7gw4"),
         // informative insert scores (insert_mode 1): transitions in LDS, match and insert scores from L2
         VIT_VARIANT(2, 0, false, true, 8, 3, false, P, "vit_s2_t0gi"),
