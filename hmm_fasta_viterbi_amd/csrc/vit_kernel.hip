@@ -138,6 +138,9 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
 #pragma unroll
             for (int q = 0; q < S; ++q) M[q] = I[q] = D[q] = NINF;
             float J = NINF, Cp = NINF;  // J exact (wave-uniform), C as per-lane partials
+            // tr_E_C == tr_E_J (the MSV specials: both logf(0.5)) makes C the same recurrence as J from the same
+            // start, so C == J bit for bit and the partials are not kept
+            const bool sameEJ = __float_as_uint(a.tr_E_C) == __float_as_uint(a.tr_E_J);
             float N = 0.0f, B = move;
             float sM = NINF, sI = NINF, sD = NINF, sMn = NINF, sDn = NINF;  // shift registers, lane 0 = -inf
             uint32_t maxcode = 0;
@@ -349,7 +352,7 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                 const float Jn = J + loop;
                 J = __builtin_expect(wave_any(E + a.tr_E_J > Jn), 0) ? fmaxf(Jn, msvk::group_max<64>(E) + a.tr_E_J)
                                                                        : Jn;
-                Cp = fmaxf(Cp + loop, E + a.tr_E_C);
+                if (!sameEJ) Cp = fmaxf(Cp + loop, E + a.tr_E_C);
                 N = N + loop;
                 B = fmaxf(N, J) + move;
             };
@@ -361,7 +364,7 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                 }
             }
             for (; i < L; ++i) row(i);
-            const float sc = msvk::group_max<64>(Cp) + move;
+            const float sc = (sameEJ ? J : msvk::group_max<64>(Cp)) + move;
             if (lane == 0) {
                 if (maxcode >= 20u) {
                     a.scores[s] = __builtin_inff();

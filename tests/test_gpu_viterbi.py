@@ -153,6 +153,29 @@ def test_long_delete_chains_cross_every_lane(prof):
         _native.lib().msv_vit_profile_destroy(p)
 
 
+@pytest.mark.parametrize("prof", ["100.hmm", "1400.hmm", "2405.hmm"])
+def test_distinct_exit_scores(prof):
+    """tr_E_C != tr_E_J (the C-ABI takes them separately): C no longer equals J, so the kernel keeps its C
+    partials; bitwise against the oracle's DP over the same tables."""
+    from hmm_fasta_viterbi_amd import _native
+    o = OracleProfile(prof)
+    _, tsc = o.vit_tables(0)
+    msc = o.emission_scores()
+    b, c, j = o.constants()
+    import ctypes as C
+    p = C.c_void_p()
+    tsc = np.ascontiguousarray(tsc, np.float32)
+    consts = (b, float(np.float32(c) - np.float32(0.75)), j)
+    assert _native.lib().msv_vit_profile_create(0, msc.ctypes.data, None, tsc.ctypes.data, o.model_length,
+                                                *consts, C.byref(p)) == 0
+    try:
+        codes, offsets = mixed_batch(prof, 67, 15, 1, 500)
+        want = vit_score_tables(msc, None, tsc, consts, codes, offsets)
+        assert np.array_equal(bits(score_custom(p, codes, offsets)), bits(want)), prof
+    finally:
+        _native.lib().msv_vit_profile_destroy(p)
+
+
 def test_empty_and_bad_residue():
     e = vit("400.hmm")
     codes, offsets = random_batch(3, 5, 0, 50)
