@@ -48,8 +48,13 @@ constexpr int kEarlyD = 8;  // slots of the unconditional first lazy-F pass befo
 __device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 
 // Lane l-1's value into lane l (64 lanes); lane 0 keeps `old`'s lane 0, which its caller keeps at -inf
-// (the dummy column k = 0).
-__device__ __forceinline__ float shift64(float last, float old) { return msvk::shift_in<64>(last, old); }
+// (the dummy column k = 0).  One DPP move across the whole wave (wave_shr:1, bound_ctrl off: the lane
+// without a source keeps `old`) instead of the row_bcast:15 + row_shr:1 pair.
+constexpr int DPP_WAVE_SHR1 = 0x138;
+__device__ __forceinline__ float shift64(float last, float old) {
+    return __int_as_float(
+        __builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(last), DPP_WAVE_SHR1, 0xF, 0xF, false));
+}
 
 }  // namespace
 
