@@ -30,6 +30,7 @@ constexpr int DPP_ROW_SHR1 = 0x111;    // row_shr:1
 constexpr int DPP_ROW_MIRROR = 0x140;  // row_mirror
 constexpr int DPP_ROW_HMIRROR = 0x141; // row_half_mirror
 constexpr int DPP_ROW_BCAST15 = 0x142; // row_bcast:15
+constexpr int DPP_WAVE_SHR1 = 0x138;   // wave_shr:1 (the whole wave, one lane down)
 
 // M_{j-1} for the first state of each lane: the last state of the previous lane of the same
 // group; -inf (the dummy M0 column, MSV_HMM.cpp:86) for the first lane of a group.  `old` supplies
@@ -51,8 +52,7 @@ __device__ __forceinline__ float shift_in(float last, float old) {
         return dpp<DPP_ROW_SHR1>(v, last);
     } else {
         static_assert(G == 64, "G must be 16, 32 or 64");
-        float v = dpp<DPP_ROW_BCAST15, 0xE>(old, last);  // rows 1-3 get lane 15 of the row before
-        return dpp<DPP_ROW_SHR1>(v, last);
+        return dpp<DPP_WAVE_SHR1>(old, last);  // one move; lane 0 has no source and keeps `old`
     }
 }
 
