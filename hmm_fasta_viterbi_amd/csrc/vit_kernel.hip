@@ -513,8 +513,12 @@ const VitVariant* vit_variants(int* count) {
         VIT_VARIANT(8, 0, false, true, 8, 3, false, P, "vit_s8_t0gi"),
         VIT_VARIANT(16, 0, false, true, 8, 3, false, P, "vit_s16_t0gi"),
         VIT_VARIANT(22, 0, false, true, 8, 3, false, P, "vit_s22_t0gi"),
+        VIT_VARIANT(28, 0, false, true, 8, 3, false, P, "vit_s28_t0gi"),
         VIT_VARIANT(32, 0, false, true, 8, 3, false, P, "vit_s32_t0gi"),
-        VIT_VARIANT(38, 0, false, true, 8, 3, false, P, "vit_s38_t0gi"),
+        VIT_VARIANT(38, 0, false, true, 8, 3, false, X, "vit_s38_t0gi"),
+        // ... one wave per SIMD where two spill (the zero-insert picks' form)
+        VIT_VARIANT(34, 7, false, true, 4, 3, false, P, "vit_s34_t7gw4i"),
+        VIT_VARIANT(38, 7, false, true, 4, 3, false, P, "vit_s38_t7gw4i"),
         VIT_VARIANT(64, 0, false, true, 8, 3, false, P, "vit_s64_t0gi"),
     };
     *count = static_cast<int>(sizeof(all) / sizeof(all[0]));

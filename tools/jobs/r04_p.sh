@@ -13,3 +13,6 @@ for r in 1 2 3; do
     MSV_LIB_PATH=$lib timeout -k 10 200 python tools/bench_reference_programs.py | sed "s#^{#{\"lib\": \"$lib\", #" >> $O/ab_reference_programs.jsonl
   done
 done
+timeout -k 10 300 python tools/vit_tune.py --profile 2405.hmm --n 3000 --lmin 300 --lmax 500 --insert-mode 1 --rounds 2 --variants vit_s38_t0gi,vit_s38_t7gw4i,vit_s64_t0gi > $O/tune_isc_2405.jsonl 2> $O/tune.err
+timeout -k 10 300 python tools/vit_tune.py --profile 2138.hmm --n 3000 --lmin 300 --lmax 500 --insert-mode 1 --rounds 2 --variants vit_s34_t7gw4i,vit_s38_t7gw4i,vit_s38_t0gi > $O/tune_isc_2138.jsonl 2>> $O/tune.err
+timeout -k 10 300 python tools/vit_tune.py --profile 1705.hmm --n 3000 --lmin 300 --lmax 500 --insert-mode 1 --rounds 2 --variants vit_s28_t0gi,vit_s32_t0gi > $O/tune_isc_1705.jsonl 2>> $O/tune.err
