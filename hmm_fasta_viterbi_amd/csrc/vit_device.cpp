@@ -482,9 +482,8 @@ msv_status msv_vit_filter_batch(msv_profile* msv, msv_vit_profile* vit, const ui
     if ((s = msv_order_longest_first(msv, vit->d_off, n, vit->d_ord, st)) != MSV_OK) return s;
     if ((s = msv_score_batch_device(msv, vit->d_res, total, vit->d_off, n, vit->d_ord, vit->d_msc_out, st)) != MSV_OK)
         return s;
-    // survivors (P <= F1) -> Viterbi, all on the device; non-survivors keep -inf
-    std::vector<float> ninf(n, kNinf);
-    VIT_HIP(hipMemcpyAsync(vit->d_sc, ninf.data(), n * sizeof(float), hipMemcpyHostToDevice, st));
+    // survivors (P <= F1) -> Viterbi, all on the device; non-survivors keep -inf (0xff800000)
+    VIT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(vit->d_sc), static_cast<int>(0xff800000u), n, st));
     // survivors listed longest first (the MSV launch's order): the Viterbi launch's tail is its shortest ones
     if ((s = msv_filter_select_device(vit->device, vit->d_msc_out, vit->d_off, vit->d_ord, n, msv_mu, msv_lambda, F1,
                                       nullptr, vit->d_sel, vit->d_words + 3, st)) != MSV_OK)
