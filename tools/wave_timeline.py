@@ -100,6 +100,17 @@ def main():
         "end_us_by_xcc_max": {int(x): round(float(end[xcc == x].max()), 1) for x in sorted(set(xcc))},
     }
     res.update(res_extra)
+    # the waves holding the batch's longest sequences (rows within 2% of the most): when they start, how fast
+    # their rows ran (the floor is their rows at the one-wave-per-SIMD row time) and how many waves shared
+    # their SIMD -- the decomposition of a latency-bound launch (cfg2) against its floor
+    lw = rows >= 0.98 * rows.max()
+    simd_key = cu_key * 4 + simd
+    _, inv, cnt = np.unique(simd_key, return_inverse=True, return_counts=True)
+    res["longest_waves"] = {
+        "count": int(lw.sum()), "rows": q(rows[lw]), "start_us_pct": q(start[lw]), "end_us_pct": q(end[lw]),
+        "ns_per_row_pct": q((end[lw] - start[lw]) * 1000.0 / np.maximum(rows[lw], 1)),
+        "waves_on_their_simd_pct": q(cnt[inv][lw]),
+    }
     print(json.dumps(res))
 
 
