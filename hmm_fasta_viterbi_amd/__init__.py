@@ -414,6 +414,10 @@ class Viterbi_HMM:
     def reserve_length(self, max_length: int) -> None:
         check(_native.lib().msv_vit_profile_reserve_length(self._p, max_length))
 
+    def bind_stream(self, stream: int | None) -> None:
+        """msv_vit_profile_bind_stream: launches on this (caller-kept-alive) stream skip the slot event."""
+        check(_native.lib().msv_vit_profile_bind_stream(self._p, stream), "msv_vit_profile_bind_stream")
+
     def check(self, stream: int | None = None) -> None:
         st = _native.lib().msv_vit_profile_check(self._p, stream)
         if st == _native.MSV_ERR_BAD_RESIDUE:

@@ -53,6 +53,7 @@ EXPORTED = [
     "msv_vit_profile_create_from_hmm", "msv_vit_profile_destroy", "msv_vit_profile_reserve_length",
     "msv_vit_profile_describe", "msv_vit_variant_count", "msv_vit_variant_name", "msv_vit_profile_set_variant",
     "msv_vit_score_batch_device", "msv_vit_score_batch", "msv_vit_profile_check", "msv_vit_filter_batch",
+    "msv_vit_profile_bind_stream",
 ]
 
 
@@ -212,6 +213,7 @@ def lib() -> C.CDLL:
         "msv_vit_variant_name": (C.c_char_p, [C.c_int]),
         "msv_vit_profile_set_variant": (C.c_int, [vp, C.c_char_p]),
         "msv_vit_score_batch_device": (C.c_int, [vp, vp, u64, vp, u64, vp, vp, vp, vp]),
+        "msv_vit_profile_bind_stream": (C.c_int, [vp, vp]),
         "msv_vit_score_batch": (C.c_int, [vp, vp, vp, u64, vp, vp]),
         "msv_vit_profile_check": (C.c_int, [vp, vp]),
         "msv_vit_filter_batch": (C.c_int, [vp, vp, vp, vp, u64, f32, f32, C.c_double, vp, vp, vp,

@@ -19,6 +19,7 @@
 #include <thread>
 #include <vector>
 
+#include "launch_ring.h"
 #include "msv.h"
 #include "msv_kernel.h"
 
@@ -182,69 +183,8 @@ const msvk::Variant* pick_variant(uint32_t states, bool narrow, bool whole_row =
     return best;
 }
 
-// Launch slots of one profile (see kLaunchSlots): the stream and completion event of each slot's
-// last launch.  An event record is a packet on the stream (~4 us between a launch and the next
-// one, 3% of a 0.14 ms cfg2 kernel), so it is recorded lazily -- only when another stream wants
-// the slot -- for streams known to outlive that moment: the library's own streams and the stream
-// the caller bound with msv_profile_bind_stream.  A launch on any other caller stream records its
-// event at once (that stream may be destroyed before the next launch).
-struct LaunchRing {
-    hipEvent_t done[kLaunchSlots] = {};
-    hipStream_t last[kLaunchSlots] = {};  // nullptr: never launched
-    bool recorded[kLaunchSlots] = {};     // done[k] covers the slot's last launch
-    bool dirty[kLaunchSlots] = {};        // a launch failed after the slot's counters were touched
-    uint32_t next = 0;
-
-    // Takes the next slot for a launch on `st`; makes `st` wait for the slot's previous launch if
-    // that ran on another stream.
-    hipError_t acquire(hipStream_t st, int* slot) {
-        const int k = static_cast<int>(next++ % kLaunchSlots);
-        if (!done[k]) {
-            // device-scope release: the event only orders this device's streams
-            const hipError_t e = hipEventCreateWithFlags(&done[k], hipEventDisableTiming | hipEventReleaseToDevice);
-            if (e != hipSuccess) return e;
-        }
-        if (last[k] && last[k] != st) {
-            // Nothing to wait for when the slot's last launch has completed: its stream is idle, or its
-            // recorded event has fired (host queries, no packets -- a fused grid call acquires a slot
-            // of every profile, and 24 record + wait pairs cost ~0.3 ms before the launch).
-            const bool finished = recorded[k] ? hipEventQuery(done[k]) == hipSuccess
-                                              : hipStreamQuery(last[k]) == hipSuccess;
-            if (!finished) {
-                if (!recorded[k]) {  // lazy: last[k] is a live stream; this covers all of its work so far
-                    const hipError_t e = hipEventRecord(done[k], last[k]);
-                    if (e != hipSuccess) return e;
-                    recorded[k] = true;
-                }
-                const hipError_t e = hipStreamWaitEvent(st, done[k], 0);
-                if (e != hipSuccess) return e;
-            }
-            (void)hipGetLastError();  // a query's hipErrorNotReady is not an error
-        }
-        *slot = k;
-        return hipSuccess;
-    }
-    // `lazy`: `st` is known to stay alive until the next acquire of this slot or flush()
-    hipError_t release(int k, hipStream_t st, bool lazy) {
-        last[k] = st;
-        recorded[k] = !lazy;
-        return lazy ? hipSuccess : hipEventRecord(done[k], st);
-    }
-    // Records the pending lazy events of stream `st` (before it stops being guaranteed alive).
-    hipError_t flush(hipStream_t st) {
-        for (int k = 0; k < kLaunchSlots; ++k)
-            if (last[k] == st && !recorded[k]) {
-                const hipError_t e = hipEventRecord(done[k], st);
-                if (e != hipSuccess) return e;
-                recorded[k] = true;
-            }
-        return hipSuccess;
-    }
-    void destroy() {
-        for (hipEvent_t& e : done)
-            if (e) (void)hipEventDestroy(e);
-    }
-};
+// Launch slots of one profile (see kLaunchSlots and launch_ring.h).
+using LaunchRing = msvrt::LaunchRing<kLaunchSlots>;
 
 }  // namespace
 
@@ -791,11 +731,10 @@ msv_status msv_profile_create(int device, const float* emission_scores, uint32_t
     // every launch slot's event up front: created lazily, the first kLaunchSlots launches of a fresh
     // profile each paid an event creation (~10 us; 24 of them in one fused grid call)
     for (LaunchRing* ring : {&p->kernels, &p->orders})
-        for (hipEvent_t& ev : ring->done)
-            if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice)) != hipSuccess) {
-                msv_profile_destroy(p);
-                return hip_status(e);
-            }
+        if ((e = ring->create_events()) != hipSuccess) {
+            msv_profile_destroy(p);
+            return hip_status(e);
+        }
     if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_words), kWords * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMemset(p->d_words, 0, kWords * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc(reinterpret_cast<void**>(&p->d_dummy), 64)) != hipSuccess ||

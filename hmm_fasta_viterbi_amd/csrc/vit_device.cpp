@@ -3,7 +3,8 @@
 // The reference parses insert emissions, transitions and STATS LOCAL VITERBI (Profile_HMM.cpp:86-87,
 // 107-120) and never scores with them.  A msv_vit_profile holds the kernel-layout tables of one compiled
 // variant (vit_kernel.hip), its own per-length {tr_loop, tr_move} table (host logf, MSV_HMM.cpp:59-64)
-// and a self-resetting dequeue counter; a batch -- typically the MSV filter's survivors, selected on the
+// and self-resetting dequeue counters (one pair per launch slot, launch_ring.h, so one profile may be
+// driven from several streams at once); a batch -- typically the MSV filter's survivors, selected on the
 // device -- is one persistent launch.
 #include <hip/hip_runtime.h>
 
@@ -15,6 +16,7 @@
 #include <new>
 #include <vector>
 
+#include "launch_ring.h"
 #include "msv.h"
 #include "msv_kernel.h"
 #include "vit_kernel.h"
@@ -23,6 +25,15 @@ namespace {
 
 constexpr uint32_t kDefaultMaxLength = 131072;
 constexpr float kNinf = -std::numeric_limits<float>::infinity();
+// d_words: [2k, 2k+1] = launch slot k's dequeue counters {next index, waves left} (zero between launches),
+// [kErrWord] = sticky error bits of device launches (msv_vit_profile_check), [kHostErrWord] = the error bits
+// of the synchronous host calls, which report and clear only their own, [kSelWord] = msv_vit_filter_batch's
+// survivors count.
+constexpr int kLaunchSlots = 8;
+constexpr int kErrWord = 2 * kLaunchSlots;
+constexpr int kHostErrWord = kErrWord + 1;
+constexpr int kSelWord = kHostErrWord + 1;
+constexpr int kWords = kSelWord + 1;
 
 struct Guard {
     int prev = -1;
@@ -52,6 +63,7 @@ msv_status hip_status(hipError_t e) {
 msv_status err_status(uint32_t err) {
     if (err & msvk::kErrBadResidue) return MSV_ERR_BAD_RESIDUE;
     if (err & msvk::kErrTooLong) return MSV_ERR_SEQUENCE_TOO_LONG;
+    if (err & msvk::kErrBadOrder) return MSV_ERR_INVALID_ARGUMENT;  // a survivors entry outside the batch
     return err ? MSV_ERR_INVALID_ARGUMENT : MSV_OK;
 }
 
@@ -84,8 +96,10 @@ struct msv_vit_profile {
     float2* d_ttab = nullptr;           // [7][S/2][64]
     float2* d_lentab = nullptr;
     uint32_t lentab_n = 0;
-    uint32_t* d_words = nullptr;        // [0, 1] dequeue counter, [2] sticky errors, [3] survivors count
+    uint32_t* d_words = nullptr;        // kWords, see kLaunchSlots
+    msvrt::LaunchRing<kLaunchSlots> kernels;  // the launch slots' streams and events
     hipStream_t stream = nullptr;
+    hipStream_t bound = nullptr;        // msv_vit_profile_bind_stream: a caller stream kept alive while bound
     // msv_vit_score_batch / msv_vit_filter_batch staging
     uint8_t* d_res = nullptr;
     size_t res_cap = 0;
@@ -196,9 +210,13 @@ hipStream_t stream_of(const msv_vit_profile* p, void* stream) {
     return stream ? static_cast<hipStream_t>(stream) : p->stream;
 }
 
+// Every launch takes the next counter slot (a slot whose previous launch ran on another stream is reused
+// only after it: launch_ring.h), so launches of one profile on several streams never share a counter.
+// `errors` is the word the kernel latches its error bits into (device launches: kErrWord; host calls:
+// kHostErrWord).
 msv_status launch(msv_vit_profile* p, const uint8_t* d_residues, const uint64_t* d_offsets, uint64_t n,
                   const uint32_t* d_select, const uint32_t* d_select_count, float* d_scores, hipStream_t st,
-                  hipEvent_t start = nullptr, hipEvent_t stop = nullptr) {
+                  uint32_t* errors, hipEvent_t start = nullptr, hipEvent_t stop = nullptr) {
     if (n == 0) return MSV_OK;
     if (n >= (1ull << 32)) return MSV_ERR_INVALID_ARGUMENT;
     vitk::VitArgs a{};
@@ -211,8 +229,7 @@ msv_status launch(msv_vit_profile* p, const uint8_t* d_residues, const uint64_t*
     a.select_count = d_select ? d_select_count : nullptr;
     a.lentab = p->d_lentab;
     a.scores = d_scores;
-    a.counter = p->d_words;
-    a.errors = p->d_words + 2;
+    a.errors = errors;
     a.n = n;
     a.lentab_n = p->lentab_n;
     a.tr_B_Mk = p->tr_B_Mk;
@@ -226,7 +243,29 @@ msv_status launch(msv_vit_profile* p, const uint8_t* d_residues, const uint64_t*
         stop = p->time_stop;
         p->time_start = p->time_stop = nullptr;
     }
-    return hip_status(vitk::vit_launch(*p->v, blocks, a, st, start, stop));
+    int k = 0;
+    VIT_HIP(p->kernels.acquire(st, &k));
+    a.counter = p->d_words + 2 * k;
+    // a slot's counters are put back to zero by the last wave of every launch; a failed launch may leave
+    // them dirty, so the slot's next launch resets them explicitly
+    if (p->kernels.dirty[k]) VIT_HIP(hipMemsetAsync(a.counter, 0, 2 * sizeof(uint32_t), st));
+    p->kernels.dirty[k] = true;
+    VIT_HIP(vitk::vit_launch(*p->v, blocks, a, st, start, stop));
+    p->kernels.dirty[k] = false;
+    VIT_HIP(p->kernels.release(k, st, st == p->stream || (p->bound && st == p->bound)));
+    return MSV_OK;
+}
+
+// Reads (and clears when set) one error word of the profile on `st`, synchronously.
+msv_status read_errors(msv_vit_profile* p, int word, hipStream_t st) {
+    uint32_t err = 0;
+    VIT_HIP(hipMemcpyAsync(&err, p->d_words + word, sizeof(err), hipMemcpyDeviceToHost, st));
+    VIT_HIP(hipStreamSynchronize(st));
+    if (err) {
+        VIT_HIP(hipMemsetAsync(p->d_words + word, 0, sizeof(uint32_t), st));
+        VIT_HIP(hipStreamSynchronize(st));
+    }
+    return err_status(err);
 }
 
 }  // namespace
@@ -242,6 +281,7 @@ void msv_vit_profile_destroy(msv_vit_profile* p) {
                     static_cast<void*>(p->d_off), static_cast<void*>(p->d_sc), static_cast<void*>(p->d_msc_out),
                     static_cast<void*>(p->d_sel), static_cast<void*>(p->d_ord)})
         (void)hipFree(d);
+    p->kernels.destroy();
     if (p->stream) (void)hipStreamDestroy(p->stream);
     delete p;
 }
@@ -277,6 +317,11 @@ msv_status msv_vit_profile_create(int device, const float* match_scores, const f
                                   float tr_E_J, msv_vit_profile** out) {
     if (!match_scores || !transition_scores || !out || model_length < 2) return MSV_ERR_INVALID_ARGUMENT;
     *out = nullptr;
+    // The kernel leaves D(LENG) out of E, exact only while every transition it reads (nodes 1 .. LENG-1,
+    // install) is <= 0 (then every D is bounded by an M of its row); log-probabilities always are.
+    for (size_t k = 1; k + 1 < model_length; ++k)
+        for (int t = 0; t < 7; ++t)
+            if (!(transition_scores[k * 7 + t] <= 0.0f)) return MSV_ERR_INVALID_ARGUMENT;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MSV_ERR_NO_DEVICE;
     if (device < 0 || device >= ndev) return MSV_ERR_NO_DEVICE;
@@ -298,8 +343,9 @@ msv_status msv_vit_profile_create(int device, const float* match_scores, const f
     p->tsc.assign(transition_scores, transition_scores + 7 * M);
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipMalloc(reinterpret_cast<void**>(&p->d_words), 8 * sizeof(uint32_t))) != hipSuccess ||
-        (e = hipMemset(p->d_words, 0, 8 * sizeof(uint32_t))) != hipSuccess) {
+        (e = p->kernels.create_events()) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void**>(&p->d_words), kWords * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMemset(p->d_words, 0, kWords * sizeof(uint32_t))) != hipSuccess) {
         msv_vit_profile_destroy(p);
         return hip_status(e);
     }
@@ -376,7 +422,19 @@ msv_status msv_vit_score_batch_device(msv_vit_profile* p, const uint8_t* d_resid
     if (d_select_count && !d_select) return MSV_ERR_INVALID_ARGUMENT;
     Guard g(p->device);
     if (!g.ok) return MSV_ERR_NO_DEVICE;
-    return launch(p, d_residues, d_offsets, n, d_select, d_select_count, d_scores, stream_of(p, stream));
+    return launch(p, d_residues, d_offsets, n, d_select, d_select_count, d_scores, stream_of(p, stream),
+                  p->d_words + kErrWord);
+}
+
+msv_status msv_vit_profile_bind_stream(msv_vit_profile* p, void* stream) {
+    if (!p) return MSV_ERR_INVALID_ARGUMENT;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (st == p->bound) return MSV_OK;
+    Guard g(p->device);
+    if (!g.ok) return MSV_ERR_NO_DEVICE;
+    if (p->bound) VIT_HIP(p->kernels.flush(p->bound));  // the old stream loses its guarantee
+    p->bound = st;
+    return MSV_OK;
 }
 
 // Diagnostic (bench.py): the next launch updates these two HIP events with its own start and end
@@ -392,13 +450,7 @@ msv_status msv_vit_profile_check(msv_vit_profile* p, void* stream) {
     if (!p) return MSV_ERR_INVALID_ARGUMENT;
     Guard g(p->device);
     if (!g.ok) return MSV_ERR_NO_DEVICE;
-    hipStream_t st = stream_of(p, stream);
-    uint32_t err = 0;
-    VIT_HIP(hipMemcpyAsync(&err, p->d_words + 2, sizeof(err), hipMemcpyDeviceToHost, st));
-    VIT_HIP(hipStreamSynchronize(st));
-    if (err) VIT_HIP(hipMemsetAsync(p->d_words + 2, 0, sizeof(uint32_t), st));
-    VIT_HIP(hipStreamSynchronize(st));
-    return err_status(err);
+    return read_errors(p, kErrWord, stream_of(p, stream));
 }
 
 msv_status msv_vit_score_batch(msv_vit_profile* p, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
@@ -423,11 +475,10 @@ msv_status msv_vit_score_batch(msv_vit_profile* p, const uint8_t* residues, cons
     VIT_HIP(ensure(p->d_sc, p->sc_cap, n));
     if (total) VIT_HIP(hipMemcpyAsync(p->d_res, residues + base, total, hipMemcpyHostToDevice, st));
     VIT_HIP(hipMemcpyAsync(p->d_off, off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    s = launch(p, p->d_res, p->d_off, n, nullptr, nullptr, p->d_sc, st);
+    s = launch(p, p->d_res, p->d_off, n, nullptr, nullptr, p->d_sc, st, p->d_words + kHostErrWord);
     if (s != MSV_OK) return s;
     VIT_HIP(hipMemcpyAsync(scores, p->d_sc, n * sizeof(float), hipMemcpyDeviceToHost, st));
-    VIT_HIP(hipStreamSynchronize(st));
-    return msv_vit_profile_check(p, st);
+    return read_errors(p, kHostErrWord, st);
 }
 
 msv_status msv_filter_select_device(int device, const float* d_scores, const uint64_t* d_offsets,
@@ -435,6 +486,9 @@ msv_status msv_filter_select_device(int device, const float* d_scores, const uin
                                     double* d_pvalues, uint32_t* d_selected, uint32_t* d_count, void* stream) {
     if (!d_count || (n && (!d_scores || !d_offsets || !d_selected))) return MSV_ERR_INVALID_ARGUMENT;
     if (n >= (1ull << 32)) return MSV_ERR_INVALID_ARGUMENT;
+    // No default stream here: NULL would be the legacy null stream, unordered with the profiles' own
+    // non-blocking streams that msv_score_batch_device / msv_vit_score_batch_device take for NULL.
+    if (!stream) return MSV_ERR_INVALID_ARGUMENT;
     Guard g(device);
     if (!g.ok) return MSV_ERR_NO_DEVICE;
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -486,13 +540,15 @@ msv_status msv_vit_filter_batch(msv_profile* msv, msv_vit_profile* vit, const ui
     VIT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(vit->d_sc), static_cast<int>(0xff800000u), n, st));
     // survivors listed longest first (the MSV launch's order): the Viterbi launch's tail is its shortest ones
     if ((s = msv_filter_select_device(vit->device, vit->d_msc_out, vit->d_off, vit->d_ord, n, msv_mu, msv_lambda, F1,
-                                      nullptr, vit->d_sel, vit->d_words + 3, st)) != MSV_OK)
+                                      nullptr, vit->d_sel, vit->d_words + kSelWord, st)) != MSV_OK)
         return s;
-    if ((s = launch(vit, vit->d_res, vit->d_off, n, vit->d_sel, vit->d_words + 3, vit->d_sc, st)) != MSV_OK) return s;
+    if ((s = launch(vit, vit->d_res, vit->d_off, n, vit->d_sel, vit->d_words + kSelWord, vit->d_sc, st,
+                    vit->d_words + kHostErrWord)) != MSV_OK)
+        return s;
     uint32_t count = 0;
     VIT_HIP(hipMemcpyAsync(msv_scores, vit->d_msc_out, n * sizeof(float), hipMemcpyDeviceToHost, st));
     VIT_HIP(hipMemcpyAsync(vit_scores, vit->d_sc, n * sizeof(float), hipMemcpyDeviceToHost, st));
-    VIT_HIP(hipMemcpyAsync(&count, vit->d_words + 3, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    VIT_HIP(hipMemcpyAsync(&count, vit->d_words + kSelWord, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     std::vector<uint32_t> sel;
     VIT_HIP(hipStreamSynchronize(st));
     if (count) {
@@ -504,7 +560,7 @@ msv_status msv_vit_filter_batch(msv_profile* msv, msv_vit_profile* vit, const ui
     for (uint32_t x : sel) passed[x] = 1;
     *n_passed = count;
     if ((s = msv_profile_check(msv, st)) != MSV_OK) return s;
-    return msv_vit_profile_check(vit, st);
+    return read_errors(vit, kHostErrWord, st);
 }
 
 }  // extern "C"

@@ -127,9 +127,12 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
     uint32_t item = blockIdx.x * WAVES + wave;
     while (item < total) {
         const uint32_t s = a.select ? a.select[item] : item;
-        const uint64_t o0 = a.offsets[s];
-        const uint64_t L = a.offsets[s + 1] - o0;
-        if (L == 0) {
+        const uint64_t o0 = a.offsets[s < a.n ? s : 0];
+        const uint64_t L = s < a.n ? a.offsets[s + 1] - o0 : 0;
+        if (s >= a.n) {
+            // a survivors entry outside the batch (a caller's list): reported, never dereferenced
+            if (lane == 0) atomicOr(a.errors, msvk::kErrBadOrder);
+        } else if (L == 0) {
             if (lane == 0) a.scores[s] = NINF;  // C_0 = -inf, as MSV_HMM.cpp:86,112
         } else if (L >= a.lentab_n) {
             if (lane == 0) {

@@ -304,7 +304,9 @@ msv_status msv_pvalues_device(int device, const float* d_scores, const uint64_t*
  * of 0..n-1, e.g. msv_order_longest_first's) is the order the survivors are listed in, up to the order in
  * which 64-entry stretches of it append (one atomic per stretch): with the longest-first permutation the
  * Viterbi launch dequeues its longest survivors first.  The survivors list feeds
- * msv_vit_score_batch_device directly (no host round trip). */
+ * msv_vit_score_batch_device directly (no host round trip).  `stream` must not be NULL
+ * (MSV_ERR_INVALID_ARGUMENT): the profiles' calls take NULL as their own non-blocking stream, which the
+ * legacy null stream does not order against, so pass the same explicit stream to the calls it chains. */
 msv_status msv_filter_select_device(int device, const float* d_scores, const uint64_t* d_offsets,
                                     const uint32_t* d_order, uint64_t n, float mu, float lambda, double threshold,
                                     double* d_pvalues, uint32_t* d_selected, uint32_t* d_count, void* stream);
@@ -346,7 +348,12 @@ msv_status msv_vit_cpu_score(const float* match_scores, const float* insert_scor
                              uint32_t model_length, float tr_B_Mk, float tr_E_C, float tr_E_J, const uint8_t* codes,
                              uint64_t L, float* score);
 
-/* Device-resident Viterbi profile.  insert_scores NULL = zero insert scores (MSV_INSERTS_ZERO). */
+/* Device-resident Viterbi profile.  insert_scores NULL = zero insert scores (MSV_INSERTS_ZERO).  Every
+ * transition score the recurrence reads (nodes 1 .. LENG-1) must be <= 0, as log-probabilities are
+ * (MSV_ERR_INVALID_ARGUMENT otherwise: the kernel relies on it to leave D(LENG) out of E).
+ * Threading, as msv_profile: one host thread at a time; from it, device launches may go to any streams
+ * (each takes its own dequeue-counter slot, reused only after that slot's previous launch), so
+ * launches of one profile on different streams may overlap. */
 msv_status msv_vit_profile_create(int device, const float* match_scores, const float* insert_scores,
                                   const float* transition_scores, uint32_t model_length, float tr_B_Mk, float tr_E_C,
                                   float tr_E_J, msv_vit_profile** out);
@@ -377,11 +384,16 @@ msv_status msv_vit_profile_set_variant(msv_vit_profile* profile, const char* nam
  * indices of the sequences to score, *d_select_count of them when d_select_count is given (a device
  * uint32, e.g. msv_filter_select_device's d_count), else n of them; NULL = every sequence.  Scores are
  * written at the sequence's index in d_scores (others untouched).  An empty sequence scores -inf; errors
- * (bad residue: +inf score, too long: NaN) are latched for msv_vit_profile_check. */
+ * (bad residue: +inf score, too long: NaN, a d_select entry >= n: skipped) are latched for
+ * msv_vit_profile_check. */
 msv_status msv_vit_score_batch_device(msv_vit_profile* profile, const uint8_t* d_residues, uint64_t residues_len,
                                       const uint64_t* d_offsets, uint64_t n, const uint32_t* d_select,
                                       const uint32_t* d_select_count, float* d_scores, void* stream);
-/* Host buffers in and out, synchronous (every sequence scored). */
+/* As msv_profile_bind_stream: `stream` is this profile's working stream until the next bind (NULL
+ * unbinds), kept alive by the caller while bound; launches on it skip the per-launch slot event. */
+msv_status msv_vit_profile_bind_stream(msv_vit_profile* profile, void* stream);
+/* Host buffers in and out, synchronous (every sequence scored); reports only its own errors (errors of
+ * earlier device launches stay latched for msv_vit_profile_check). */
 msv_status msv_vit_score_batch(msv_vit_profile* profile, const uint8_t* residues, const uint64_t* offsets, uint64_t n,
                                float* scores, void* stream);
 msv_status msv_vit_profile_check(msv_vit_profile* profile, void* stream);

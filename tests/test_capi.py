@@ -95,3 +95,25 @@ def test_host_only_entry_points_validate_arguments():
     assert L.msv_fasta_device_count(None) == 0 and L.msv_fasta_device_codes(None) is None
     assert L.msv_score_fasta_device(None, None, None) == 1
     assert L.msv_fasta_device_device(None) == -1  # no set: no device
+
+
+def test_viterbi_entry_points_validate_arguments():
+    """a positive transition score (the kernel leaves D(LENG) out of E, exact only for
+    transitions <= 0) and a NULL stream for msv_filter_select_device (the legacy null stream, unordered
+    with the profiles' non-blocking streams) are rejected before any device is touched."""
+    import numpy as np
+    L = _native.lib()
+    M = 101
+    msc = np.zeros((20, M), np.float32)
+    tsc = np.full((M, 7), np.float32(np.log(np.float32(0.5))), np.float32)
+    tsc[5, 3] = 0.25  # node 5, i->m
+    p = C.c_void_p()
+    assert L.msv_vit_profile_create(0, msc.ctypes.data, None, tsc.ctypes.data, M, -8.0, -0.69, -0.69,
+                                    C.byref(p)) == 1
+    tsc[5, 3] = np.nan
+    assert L.msv_vit_profile_create(0, msc.ctypes.data, None, tsc.ctypes.data, M, -8.0, -0.69, -0.69,
+                                    C.byref(p)) == 1
+    cnt = np.zeros(1, np.uint32)  # never dereferenced: the stream check comes first
+    assert L.msv_filter_select_device(0, None, None, None, 0, -9.0, 0.7, 0.02, None, None, cnt.ctypes.data,
+                                      None) == 1
+    assert L.msv_vit_profile_bind_stream(None, None) == 1

@@ -444,6 +444,27 @@ def test_pvalues_match_every_profiles_calibration():
             assert t / 2.5 < float(np.mean(pv < t)) < t * 2.5, (prof, t, float(np.mean(pv < t)))
 
 
+@pytest.mark.parametrize("length,n", [(400, 10_000), (2000, 2_500)])
+def test_pvalues_calibrated_at_the_bench_lengths(length, n):
+    """the MSV filter where it is used -- iid background sequences of the bench's
+    lengths (cfg3 ~400, cfg5 ~2000), not only HMMER's L = 200 sample -- still give ~uniform P-values and a
+    refitted mu within 0.75 bits on all 24 profiles: the per-length N/C/J loops and null1 carry the
+    calibration across lengths (profiles/r05_filter_length_composition.jsonl).  The bench's survivor
+    fraction (7% cfg3, 11% cfg5 at F1 = 0.02) comes from its uniform-letter composition, not from length
+    (tests/test_filter_composition.py)."""
+    from hmm_fasta_viterbi_amd.synthetic import background_batch
+    codes, offsets = background_batch(2024 + length, n, length)
+    for prof in PROFILES:
+        e = engine(prof)
+        pv = e.pvalues(e.score_batch(codes=codes, offsets=offsets), offsets)
+        mu, lam = e.msv_mu, e.msv_lambda
+        b = mu - np.log(-np.log1p(-pv)) / lam
+        mu_fit = -np.log(np.mean(np.exp(-lam * b))) / lam
+        assert abs(mu_fit - mu) < 0.75, (prof, length, mu, mu_fit)
+        for t in (0.5, 0.1, 0.01):
+            assert t / 2.5 < float(np.mean(pv < t)) < t * 2.5, (prof, length, t, float(np.mean(pv < t)))
+
+
 def test_pvalues_device_matches_host():
     """the device P-value kernel equals the host formula (float64 libm vs device
     libm: 1e-13 relative), on GPU scores of a seeded batch, and msv_filter's pass mask uses it."""
