@@ -25,6 +25,7 @@ constexpr int kClockTwin = -1;
 constexpr uint32_t kErrBadResidue = 1u;
 constexpr uint32_t kErrTooLong = 2u;
 constexpr uint32_t kErrBadOrder = 4u;  // a dequeue-order entry >= n (caller's order, or a poisoned sort)
+constexpr uint32_t kErrTeamHang = 8u;  // a Viterbi team's LDS exchange never completed (vit_team.hip; a bug)
 
 // Residue rows of the [row][chunk][lane] float4 table that fit the 160 KiB LDS of one CU.
 constexpr int lds_rows_for(int G, int S) {

@@ -64,6 +64,7 @@ msv_status err_status(uint32_t err) {
     if (err & msvk::kErrBadResidue) return MSV_ERR_BAD_RESIDUE;
     if (err & msvk::kErrTooLong) return MSV_ERR_SEQUENCE_TOO_LONG;
     if (err & msvk::kErrBadOrder) return MSV_ERR_INVALID_ARGUMENT;  // a survivors entry outside the batch
+    if (err & msvk::kErrTeamHang) return MSV_ERR_HIP;
     return err ? MSV_ERR_INVALID_ARGUMENT : MSV_OK;
 }
 
@@ -76,7 +77,7 @@ const vitk::VitVariant* pick_variant(uint32_t states, bool isc) {
     for (int i = 0; i < n; ++i) {
         const vitk::VitVariant& v = all[i];
         if (!v.pick || v.isc != isc || static_cast<uint32_t>(v.states()) < states) continue;
-        if (!best || v.S < best->S) best = &v;
+        if (!best || v.states() < best->states()) best = &v;
     }
     return best;
 }
@@ -130,10 +131,11 @@ hipError_t ensure(T*& p, size_t& cap, size_t need) {
     return e;
 }
 
-// Kernel layouts of the variant's tables (vit_kernel.h): slot q of lane l is state k = l * S + q + 1;
-// chunk c of a lane holds slots 2c, 2c + 1 as one float2, lanes contiguous.
+// Kernel layouts of the variant's tables (vit_kernel.h): slot q of (virtual) lane l is state k = l * S + q + 1;
+// chunk c of a lane holds slots 2c, 2c + 1 as one float2, lanes contiguous (a team's 64 * team virtual lanes;
+// an odd S leaves the last chunk's second slot unused).
 msv_status install(msv_vit_profile* p, const vitk::VitVariant* v) {
-    const int S = v->S, C2 = S / 2, L64 = vitk::kLanes;
+    const int S = v->S, C2 = v->chunks(), L64 = vitk::kLanes * v->team;
     const uint32_t M = p->model_length, K = M - 1;
     const size_t row2 = static_cast<size_t>(C2) * L64;
     auto state = [&](int l, int q) -> uint32_t { return static_cast<uint32_t>(l * S + q + 1); };
@@ -143,7 +145,7 @@ msv_status install(msv_vit_profile* p, const vitk::VitVariant* v) {
             for (int l = 0; l < L64; ++l) {
                 float e2[2], i2[2];
                 for (int h = 0; h < 2; ++h) {
-                    const uint32_t k = state(l, 2 * c + h);
+                    const uint32_t k = 2 * c + h < S ? state(l, 2 * c + h) : K + 1;  // (unused slot)
                     e2[h] = k <= K ? p->msc[static_cast<size_t>(r) * M + k] : kNinf;
                     i2[h] = (p->isc && k < K) ? p->isc_tab[static_cast<size_t>(r) * M + k] : 0.0f;
                 }
@@ -170,7 +172,8 @@ msv_status install(msv_vit_profile* p, const vitk::VitVariant* v) {
     for (int j = 0; j < vitk::kTransitions; ++j)
         for (int c = 0; c < C2; ++c)
             for (int l = 0; l < L64; ++l)
-                tt[(j * C2 + c) * L64 + l] = make_float2(slot_t(j, state(l, 2 * c)), slot_t(j, state(l, 2 * c + 1)));
+                tt[(j * C2 + c) * L64 + l] = make_float2(slot_t(j, state(l, 2 * c)),
+                                                         slot_t(j, 2 * c + 1 < S ? state(l, 2 * c + 1) : K + 1));
 
     float2 *de = nullptr, *di = nullptr, *dt = nullptr;
     hipError_t e;
@@ -235,8 +238,9 @@ msv_status launch(msv_vit_profile* p, const uint8_t* d_residues, const uint64_t*
     a.tr_B_Mk = p->tr_B_Mk;
     a.tr_E_C = p->tr_E_C;
     a.tr_E_J = p->tr_E_J;
-    // one wave per sequence: no more workgroups than the items need (a device count is bounded by n)
-    const uint64_t need = (n + p->v->waves - 1) / p->v->waves;
+    // one wave (team) per sequence: no more workgroups than the items need (a device count is bounded by n)
+    const uint64_t per_block = static_cast<uint64_t>(p->v->sequences_per_block());
+    const uint64_t need = (n + per_block - 1) / per_block;
     const uint32_t blocks = static_cast<uint32_t>(std::min<uint64_t>(p->blocks, need));
     if (!start && !stop && (p->time_start || p->time_stop)) {
         start = p->time_start;
@@ -379,6 +383,7 @@ msv_status msv_vit_profile_describe(const msv_vit_profile* p, msv_vit_info* out)
     out->match_in_lds = p->v->elds ? 1u : 0u;
     out->insert_scores = p->v->isc ? 1u : 0u;
     out->waves_per_block = static_cast<uint32_t>(p->v->waves);
+    out->waves_per_sequence = static_cast<uint32_t>(p->v->team);
     out->blocks = p->blocks;
     out->lds_bytes = static_cast<uint32_t>(p->v->lds_bytes);
     out->max_length = p->lentab_n ? p->lentab_n - 1 : 0;

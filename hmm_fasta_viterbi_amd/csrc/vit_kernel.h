@@ -41,19 +41,27 @@ struct VitArgs {
 // row, informative insert scores (isc, read from L2) or HMMER3's zero insert scores; `waves` 64-lane waves
 // per workgroup.  `pick`: the automatic choice for its S (one per S and insert mode, chosen by measurement,
 // profiles/r04_vit_tune_*.jsonl); the others are A/B candidates reachable through msv_vit_profile_set_variant.
+//
+// team > 1 (vit_team.hip, round 5): one sequence per TEAM of `team` waves (virtual lane v = w * 64 + lane
+// holds states v * S + 1 .. v * S + S; the tables' lane axis is the team's 64 * team virtual lanes), with
+// waves / team teams per workgroup.
 struct VitVariant {
     int S;
     int ntreg;
     bool elds, isc;
-    int waves;
+    int waves;  // per workgroup
     bool pick;
     const void* fn;
     const char* name;
     int lds_bytes;
-    int states() const { return kLanes * S; }
+    int team = 1;  // waves per sequence
+    int states() const { return kLanes * S * team; }
+    int chunks() const { return (S + 1) / 2; }      // float2 chunks per lane in the table layouts
+    int sequences_per_block() const { return waves / team; }
 };
 
-const VitVariant* vit_variants(int* count);
+const VitVariant* vit_variants(int* count);      // every variant: vit_kernel.hip's, then the team family
+const VitVariant* vit_team_variants(int* count);  // vit_team.hip
 hipError_t vit_launch(const VitVariant& v, uint32_t blocks, const VitArgs& args, hipStream_t stream,
                       hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 // MSV filter survivors: P-value of every MSV score (msv_pvalue_of, STATS LOCAL MSV), written to pvalues

@@ -33,6 +33,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <vector>
 
 #include "msv_kernel_impl.h"
@@ -457,7 +458,7 @@ hipError_t launch_select(const float* scores, const uint64_t* offsets, const uin
 // profiles/r04_vit_tune_cfg{2,3,5}.jsonl); `-` are the A/B candidates kept selectable by name.
 #define P true
 #define X false
-const VitVariant* vit_variants(int* count) {
+static const VitVariant* single_wave_variants(int* count) {
     static const VitVariant all[] = {
         // every transition array in VGPRs, match scores in LDS
         VIT_VARIANT(2, 7, true, false, 8, 0, false, P, "vit_s2_t7"),
@@ -529,6 +530,20 @@ const VitVariant* vit_variants(int* count) {
 }
 #undef P
 #undef X
+
+const VitVariant* vit_variants(int* count) {
+    static std::vector<VitVariant> all;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        int n1 = 0, n2 = 0;
+        const VitVariant* a1 = single_wave_variants(&n1);
+        const VitVariant* a2 = vit_team_variants(&n2);
+        all.assign(a1, a1 + n1);
+        all.insert(all.end(), a2, a2 + n2);
+    });
+    *count = static_cast<int>(all.size());
+    return all.data();
+}
 
 hipError_t vit_launch(const VitVariant& v, uint32_t blocks, const VitArgs& args, hipStream_t stream, hipEvent_t start,
                       hipEvent_t stop) {

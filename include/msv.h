@@ -372,6 +372,7 @@ typedef struct msv_vit_info {
     uint32_t lds_bytes;
     uint32_t max_length;
     int device;
+    uint32_t waves_per_sequence; /* 1, or a team of waves sharing one sequence's row (vit_team.hip) */
     char variant[64];
 } msv_vit_info;
 msv_status msv_vit_profile_describe(const msv_vit_profile* profile, msv_vit_info* out);

@@ -72,9 +72,11 @@ def test_run_on_sequence_cpu_and_gpu_agree():
 def test_every_variant(name):
     """Every compiled instantiation (S, transitions in VGPRs / LDS, match scores in LDS / L2, insert
     scores) forced on the profiles it covers, against the oracle."""
-    S = int(name.split("_")[1][1:])
+    import re
+    m = re.match(r"vit_(?:w(\d+)_)?s(\d+)_", name)
+    states = 64 * int(m.group(2)) * int(m.group(1) or 1)  # team variants: W waves of 64 lanes x S states
     isc = name.endswith("i")
-    cover = [p for p in PROFILES if int(p.split(".")[0]) <= 64 * S]
+    cover = [p for p in PROFILES if int(p.split(".")[0]) <= states]
     profs = sorted({cover[-1], cover[len(cover) // 2], cover[0]}, key=lambda p: int(p.split(".")[0]))
     for prof in profs:
         e = msv.Viterbi_HMM(hmm(prof), insert_mode=1 if isc else 0)
