@@ -74,11 +74,16 @@ struct TeamX {
 // record is ONE ds_write (its stamp rides with the data: a reader that sees the stamp sees the record).
 typedef float v2f __attribute__((ext_vector_type(2)));
 typedef float v4f __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ v4f lds_read4(const float4* p) { return *reinterpret_cast<const volatile v4f*>(p); }
-__device__ __forceinline__ v2f lds_read2(const float2* p) { return *reinterpret_cast<const volatile v2f*>(p); }
-__device__ __forceinline__ void lds_write4(float4* p, v4f v) { *reinterpret_cast<volatile v4f*>(p) = v; }
-__device__ __forceinline__ void lds_write2(float2* p, v2f v) { *reinterpret_cast<volatile v2f*>(p) = v; }
+#define LDS_AS __attribute__((address_space(3)))
+__device__ __forceinline__ v4f lds_read4(const float4* p) { return *(const volatile LDS_AS v4f*)(p); }
+__device__ __forceinline__ v2f lds_read2(const float2* p) { return *(const volatile LDS_AS v2f*)(p); }
+__device__ __forceinline__ void lds_write4(float4* p, v4f v) { *(volatile LDS_AS v4f*)(p) = v; }
+__device__ __forceinline__ void lds_write2(float2* p, v2f v) { *(volatile LDS_AS v2f*)(p) = v; }
 __device__ __forceinline__ uint32_t ufirst(float x) { return __builtin_amdgcn_readfirstlane(__float_as_uint(x)); }
+__device__ __forceinline__ uint64_t u64first(uint64_t x) {
+    return (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32))) << 32) |
+           __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));
+}
 
 }  // namespace
 
@@ -93,7 +98,8 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     __shared__ float2 etab_s[ELDS ? kRows * ROW2 : 1];
     __shared__ TeamX<W> tx_s[NT];
     const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
+    // (readfirstlane: the wave's index is wave-uniform, so branches on it are scalar)
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int team = wv / W, w = wv % W;
     const int vl = w * kLanes + lane;
     TeamX<W>& tx = tx_s[team];
@@ -128,7 +134,8 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
         if (lane == 0) lds_write2(&tx.e[st & 1][w], v2f{Ew, __uint_as_float(st)});
     };
     bool hung = false;
-    auto wait_e = [&](float Ew, uint32_t st) -> float {
+    auto wait_e = [&](float Ew, uint32_t st_) -> float {
+        const uint32_t st = __builtin_amdgcn_readfirstlane(st_);  // (keeps the stamp compare scalar)
         float m = Ew;
 #pragma unroll
         for (int o = 1; o < W; ++o) {
@@ -147,9 +154,11 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     while (item < total) {
         uint32_t tnext = 0;
         if (leader) tnext = atomicAdd(a.counter, 1u);  // the team's next sequence, published at this one's end
-        const uint32_t s = a.select ? a.select[item] : item;
-        const uint64_t o0 = a.offsets[s < a.n ? s : 0];
-        const uint64_t L = s < a.n ? a.offsets[s + 1] - o0 : 0;
+        // (readfirstlane: the sequence, its bounds and so every branch on them are wave-uniform -- scalar
+        // branches and a scalar row counter, not exec-masked regions)
+        const uint32_t s = __builtin_amdgcn_readfirstlane(a.select ? a.select[item] : item);
+        const uint64_t o0 = u64first(a.offsets[s < a.n ? s : 0]);
+        const uint64_t L = s < a.n ? u64first(a.offsets[s + 1]) - o0 : 0;
         if (s >= a.n || L == 0 || L >= a.lentab_n) {
             if (leader) {
                 if (s >= a.n) {
@@ -244,9 +253,13 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                     I[q] = inew;
                 }
                 I[0] = fmaxf(M[0] + tr[MI][0], I[0] + tr[II][0]);
+                // pin phase A here, ahead of the polls (left alone, the compiler sinks it past them to its uses
+                // in phase B, and the hop is waited for with nothing to issue)
+#pragma unroll
+                for (int q = 0; q < S; ++q) asm volatile("" : "+v"(M[q]), "+v"(I[q]));
                 // ---- exchange of row i-1 (stamp rc-1)
                 if (i != 0) {
-                    const uint32_t st = rc - 1;
+                    const uint32_t st = __builtin_amdgcn_readfirstlane(rc - 1);
                     if (w > 0) {
                         // the left wave's boundary (its D chain final), then this wave's lazy-F of row i-1:
                         // its own lane boundaries and, in lane 0, D(k0) = max(M_left + tMD, D_left + tDD)
@@ -378,12 +391,24 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
 
 const VitVariant* vit_team_variants(int* count) {
     static const VitVariant all[] = {
+        // three waves per SIMD (<= 168 VGPRs): 12-wave workgroups of 6 teams
         VIT_TEAM(2, 11, true, 6, false, "vit_w2_s11_e"),
         VIT_TEAM(2, 11, false, 6, false, "vit_w2_s11_g"),
         VIT_TEAM(2, 12, true, 6, false, "vit_w2_s12_e"),
-        VIT_TEAM(2, 19, false, 4, false, "vit_w2_s19_g"),
-        VIT_TEAM(3, 13, false, 2, false, "vit_w3_s13_g"),
+        VIT_TEAM(2, 12, false, 6, true, "vit_w2_s12_g"),
         VIT_TEAM(4, 10, false, 3, false, "vit_w4_s10_g"),
+        // two waves per SIMD (<= 256 VGPRs): 8-wave workgroups of 4 teams; match scores in LDS while the
+        // table fits (S <= 14), else from L2
+        VIT_TEAM(2, 13, true, 4, false, "vit_w2_s13_e"),
+        VIT_TEAM(2, 14, true, 4, false, "vit_w2_s14_e"),
+        VIT_TEAM(2, 13, false, 4, false, "vit_w2_s13_g"),
+        VIT_TEAM(2, 14, false, 4, false, "vit_w2_s14_g"),
+        VIT_TEAM(2, 15, false, 4, true, "vit_w2_s15_g"),
+        VIT_TEAM(2, 16, false, 4, false, "vit_w2_s16_g"),
+        VIT_TEAM(2, 17, false, 4, true, "vit_w2_s17_g"),
+        VIT_TEAM(2, 18, false, 4, true, "vit_w2_s18_g"),
+        VIT_TEAM(2, 19, false, 4, true, "vit_w2_s19_g"),
+        VIT_TEAM(3, 13, false, 2, false, "vit_w3_s13_g"),
     };
     *count = static_cast<int>(sizeof(all) / sizeof(all[0]));
     return all;

@@ -384,3 +384,43 @@ def test_viterbi_pvalues_calibrated_at_the_bench_lengths(length, n):
         assert -0.3 < mu_fit - mu < 0.9, (prof, length, mu, mu_fit)
         for t in (0.5, 0.1, 0.01):
             assert t / 2.5 < float(np.mean(pv < t)) < t * 2.5, (prof, length, t, float(np.mean(pv < t)))
+
+
+TEAM_VARIANTS = [v for v in msv.Viterbi_HMM.variants() if v.startswith("vit_w")]
+
+
+@pytest.mark.parametrize("name", TEAM_VARIANTS)
+def test_team_variant_stress(name):
+    """The team kernels (vit_team.hip: one sequence over W waves, LDS exchange per row) on the cases that
+    exercise the exchange: the lazy-F stress model (D chains crossing many lanes AND the waves' boundaries),
+    distinct exit scores (per-lane C partials reduced across the team), and a batch mixing empty, 1-residue,
+    bad-length and long sequences -- bitwise against the oracle's DP over the same tables."""
+    import re
+    from hmm_fasta_viterbi_amd import _native
+    m = re.match(r"vit_w(\d+)_s(\d+)_", name)
+    states = 64 * int(m.group(1)) * int(m.group(2))
+    prof = [p for p in PROFILES if int(p.split(".")[0]) <= states][-1]
+    o = OracleProfile(prof)
+    _, tsc0 = o.vit_tables(0)
+    msc = o.emission_scores()
+    b, c, j = o.constants()
+    stress = tsc0.copy()
+    stress[:, 6] = np.float32(np.log(np.float32(0.995)))
+    stress[:, 2] = np.float32(np.log(np.float32(0.3)))
+    stress[:, 5] = np.float32(np.log(np.float32(0.9)))
+    for tsc, consts in ((stress, (b, c, j)), (tsc0, (b, float(np.float32(c) - np.float32(0.75)), j))):
+        p, _, _ = custom_profile(prof, tsc) if consts == (b, c, j) else (None, None, None)
+        if p is None:
+            import ctypes as C
+            p = C.c_void_p()
+            t = np.ascontiguousarray(tsc, np.float32)
+            assert _native.lib().msv_vit_profile_create(0, msc.ctypes.data, None, t.ctypes.data, o.model_length,
+                                                        *consts, C.byref(p)) == 0
+        try:
+            assert _native.lib().msv_vit_profile_set_variant(p, name.encode()) == 0
+            codes, offsets = concat_batches((np.zeros(0, np.uint8), np.zeros(3, np.uint64)),
+                                            mixed_batch(prof, 73, 12, 1, 700))
+            want = vit_score_tables(msc, None, tsc, consts, codes, offsets)
+            assert np.array_equal(bits(score_custom(p, codes, offsets)), bits(want)), (name, prof, consts)
+        finally:
+            _native.lib().msv_vit_profile_destroy(p)

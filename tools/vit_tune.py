@@ -69,8 +69,14 @@ def main():
     leng = h.model_length - 1
     cells = int(offsets[-1]) * leng
     vit = msv.Viterbi_HMM(h, insert_mode=a.insert_mode)
+    import re
+
+    def states(v):  # team variants vit_w<W>_s<S>_*: W waves of 64 lanes x S states
+        m = re.match(r"vit_(?:w(\d+)_)?s(\d+)_", v)
+        return 64 * int(m.group(2)) * int(m.group(1) or 1)
+
     names = a.variants.split(",") if a.variants else [
-        v for v in vit.variants() if (v.endswith("i") == bool(a.insert_mode)) and 64 * int(v.split("_")[1][1:]) >= leng]
+        v for v in vit.variants() if (v.endswith("i") == bool(a.insert_mode)) and states(v) >= leng]
     dev = torch.device("cuda:0")
     st = torch.cuda.Stream(dev)
     r = torch.from_numpy(codes).to(dev)
