@@ -47,6 +47,10 @@ constexpr float NINF = -__builtin_inff();
 constexpr int kEarlyD = 8;  // slots of the unconditional first lazy-F pass before its early-exit test
 
 __device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+__device__ __forceinline__ uint64_t u64first(uint64_t x) {
+    return (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32))) << 32) |
+           __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));
+}
 
 // Lane l-1's value into lane l (64 lanes); lane 0 keeps `old`'s lane 0, which its caller keeps at -inf
 // (the dummy column k = 0).  One DPP move across the whole wave (wave_shr:1, bound_ctrl off: the lane
@@ -90,7 +94,8 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
     __shared__ float2 etab_s[ELDS ? kRows * ROW2 : 1];
     __shared__ float2 ttab_s[NTL ? NTL * ROW2 : 1];
     const int lane = threadIdx.x & 63;
-    const uint32_t wave = threadIdx.x >> 6;
+    // (readfirstlane: wave-uniform, so the sequence, its bounds and every branch on them are scalar)
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
     if constexpr (ELDS)
         for (int i = threadIdx.x; i < kRows * ROW2; i += WAVES * 64) etab_s[i] = a.etab[i];
@@ -127,9 +132,9 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
     const uint32_t nwaves = gridDim.x * WAVES;
     uint32_t item = blockIdx.x * WAVES + wave;
     while (item < total) {
-        const uint32_t s = a.select ? a.select[item] : item;
-        const uint64_t o0 = a.offsets[s < a.n ? s : 0];
-        const uint64_t L = s < a.n ? a.offsets[s + 1] - o0 : 0;
+        const uint32_t s = __builtin_amdgcn_readfirstlane(a.select ? a.select[item] : item);
+        const uint64_t o0 = u64first(a.offsets[s < a.n ? s : 0]);
+        const uint64_t L = s < a.n ? u64first(a.offsets[s + 1]) - o0 : 0;
         if (s >= a.n) {
             // a survivors entry outside the batch (a caller's list): reported, never dereferenced
             if (lane == 0) atomicOr(a.errors, msvk::kErrBadOrder);

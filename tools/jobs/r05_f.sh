@@ -16,3 +16,5 @@ for g in "SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" "SQ_WAIT_ANY SQ
 done
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pmc/trace -o run -- python3 tools/run_vit.py --config cfg5 --launches 2 >> $O/pmc.log 2>&1
 python3 tools/pmc_summary.py $O/pmc cfg5_viterbi vit_team_kernel > $O/pmc_cfg5.json
+# the single-wave kernels with wave-uniform sequence state (readfirstlane), A/B against the committed build
+timeout -k 10 400 python tools/vit_ab.py --config cfg3 --variant vit_s22_t5a --rounds 3 abx/base/libmsv_hip.so abx/new/libmsv_hip.so > $O/ab_uniform_cfg3.jsonl
