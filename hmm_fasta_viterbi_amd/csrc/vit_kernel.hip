@@ -461,9 +461,10 @@ hipError_t launch_select(const float* scores, const uint64_t* offsets, const uin
 
 // `P` marks the automatic choice per S (interleaved timings on the MSV survivors of cfg3 / cfg5 and on cfg2,
 // profiles/r04_vit_tune_cfg{2,3,5}.jsonl); `-` are the A/B candidates kept selectable by name.  Round 5: the
-// team variants (vit_team.hip) took over 1,409-1,536, 1,793-1,920 and 2,049-2,432 states
+// team variants (vit_team.hip) took over 1,409-1,920 and 2,049-2,432 states
 // (profiles/r05_team_tune_bands.jsonl: 1509.hmm 2.02 vs 2.23 ms, 1901.hmm 2.78 vs 2.82, 2050-2365.hmm
-// 27-32% faster; cfg5's survivors 22.2 vs 33.7 ms), so s24_t0g, s30_t0g and s34/36/38_t7gw4 are no longer picks.
+// 27-32% faster; cfg5's survivors 22.2 vs 33.7 ms; 1600 / 1705.hmm -4 / -6%, profiles/r05_team_tune_bands_s13s14.jsonl),
+// so s24..s30_t0g and s34/36/38_t7gw4 are no longer picks.
 #define P true
 #define X false
 static const VitVariant* single_wave_variants(int* count) {
@@ -489,8 +490,8 @@ static const VitVariant* single_wave_variants(int* count) {
         VIT_VARIANT(22, 0, true, false, 8, 1, false, X, "vit_s22_t0"),
         // transitions in LDS, match scores from L2
         VIT_VARIANT(24, 0, false, false, 8, 3, false, X, "vit_s24_t0g"),
-        VIT_VARIANT(26, 0, false, false, 8, 3, false, P, "vit_s26_t0g"),
-        VIT_VARIANT(28, 0, false, false, 8, 3, false, P, "vit_s28_t0g"),
+        VIT_VARIANT(26, 0, false, false, 8, 3, false, X, "vit_s26_t0g"),
+        VIT_VARIANT(28, 0, false, false, 8, 3, false, X, "vit_s28_t0g"),
         VIT_VARIANT(30, 0, false, false, 8, 3, false, X, "vit_s30_t0g"),
         VIT_VARIANT(32, 0, false, false, 8, 3, false, P, "vit_s32_t0g"),
         VIT_VARIANT(38, 0, false, false, 8, 3, false, X, "vit_s38_t0g"),

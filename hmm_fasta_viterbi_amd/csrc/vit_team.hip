@@ -88,14 +88,20 @@ __device__ __forceinline__ uint64_t u64first(uint64_t x) {
 }  // namespace
 
 // W waves per sequence, S states per lane (any S >= 2), match scores staged in LDS (ELDS) or read from L2
-// each row (prefetched a row ahead), NT teams per workgroup.  Transitions: all seven arrays in VGPRs.
-template <int W, int S, bool ELDS, int NT>
+// each row, NT teams per workgroup.  Transitions: all seven arrays in VGPRs, or (LA = 1) the four of
+// phase A (MM_IN, IM_IN, MI, II) in LDS, read chunk by chunk in phase A -- 4 S fewer VGPRs, so that the
+// two-wave teams fit three waves per SIMD; LA = 2 also DM_IN (phase B, read a chunk ahead).  DD_IN and
+// MD_IN (the D chain and lazy-F) stay in VGPRs.
+template <int W, int S, bool ELDS, int NT, int LA = 0>
 __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) {
     static_assert(S >= 2 && W >= 2 && W <= 4, "team shape");
     constexpr int C2 = (S + 1) / 2;  // float2 chunks per lane (an odd S leaves the last .y unused)
     constexpr int VL = W * kLanes;   // virtual lanes of a team
     constexpr int ROW2 = C2 * VL;    // float2 per table row
+    // transition arrays in LDS: MM_IN, IM_IN, MI, II (LDS slots 0 .. 3), and DM_IN (slot 4, LA = 2)
+    constexpr int NLA = LA == 2 ? 5 : LA == 1 ? 4 : 0;
     __shared__ float2 etab_s[ELDS ? kRows * ROW2 : 1];
+    __shared__ float2 ttab_s[LA ? NLA * C2 * VL : 1];
     __shared__ TeamX<W> tx_s[NT];
     const int lane = threadIdx.x & 63;
     // (readfirstlane: the wave's index is wave-uniform, so branches on it are scalar)
@@ -106,19 +112,30 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
 
     if constexpr (ELDS)
         for (int i = threadIdx.x; i < kRows * ROW2; i += NT * W * 64) etab_s[i] = a.etab[i];
+    if constexpr (LA) {
+        constexpr int la_src[5] = {MM_IN, IM_IN, MI, II, DM_IN};
+        for (int i = threadIdx.x; i < NLA * C2 * VL; i += NT * W * 64)
+            ttab_s[i] = a.ttab[la_src[i / (C2 * VL)] * C2 * VL + i % (C2 * VL)];
+    }
     for (int i = threadIdx.x; i < static_cast<int>(NT * sizeof(TeamX<W>) / 4); i += NT * W * 64)
         reinterpret_cast<uint32_t*>(tx_s)[i] = 0xFFFFFFFFu;  // no stamp matches
     __syncthreads();
 
     float tr[kTransitions][S];
 #pragma unroll
-    for (int j = 0; j < kTransitions; ++j)
+    for (int j = 0; j < kTransitions; ++j) {
+        if (LA && (j == MM_IN || j == IM_IN || j == MI || j == II)) continue;
+        if (LA == 2 && j == DM_IN) continue;
 #pragma unroll
         for (int c = 0; c < C2; ++c) {
             const float2 t = a.ttab[(j * C2 + c) * VL + vl];
             tr[j][2 * c] = t.x;
             if (2 * c + 1 < S) tr[j][2 * c + 1] = t.y;
         }
+    }
+    // LA: an opaque zero renewed every row keeps the compiler from hoisting the loop-invariant LDS reads of
+    // the phase-A arrays out of the row loop into VGPRs (which would undo them)
+    uint32_t rz = 0;
 
     const uint64_t total = a.select_count ? static_cast<uint64_t>(*a.select_count) : a.n;
     const uint32_t nteams = gridDim.x * NT;
@@ -246,13 +263,43 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                 }
                 // ---- phase A (the previous row's own values only): I(i, .), and a_q = max(M'(q-1)+tMM,
                 // I'(q-1)+tIM) in place of M'(q) (M'(q) is dead once I(i, q) and a_{q+1} are made)
+                if constexpr (LA) {
+                    // chunk by chunk, highest first; each chunk's four pairs read one chunk ahead
+                    asm volatile("" : "+v"(rz));
+                    const float2* tl = ttab_s + rz + vl;
+                    auto ld = [&](int c, float2 (&t)[4]) {
 #pragma unroll
-                for (int q = S - 1; q >= 1; --q) {
-                    const float inew = fmaxf(M[q] + tr[MI][q], I[q] + tr[II][q]);
-                    M[q] = fmaxf(M[q - 1] + tr[MM_IN][q], I[q - 1] + tr[IM_IN][q]);
-                    I[q] = inew;
+                        for (int j = 0; j < 4; ++j) t[j] = tl[(j * C2 + c) * VL];
+                    };
+                    float2 tc[4], tn[4];
+                    ld(C2 - 1, tc);
+#pragma unroll
+                    for (int c = C2 - 1; c >= 0; --c) {
+                        if (c > 0) ld(c - 1, tn);
+#pragma unroll
+                        for (int h = 1; h >= 0; --h) {
+                            const int q = 2 * c + h;
+                            if (q >= S) continue;
+                            const float tmm = h ? tc[0].y : tc[0].x, tim = h ? tc[1].y : tc[1].x;
+                            const float tmi = h ? tc[2].y : tc[2].x, tii = h ? tc[3].y : tc[3].x;
+                            const float inew = fmaxf(M[q] + tmi, I[q] + tii);
+                            if (q >= 1) M[q] = fmaxf(M[q - 1] + tmm, I[q - 1] + tim);
+                            I[q] = inew;
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (c > 0)
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) tc[j] = tn[j];
+                    }
+                } else {
+#pragma unroll
+                    for (int q = S - 1; q >= 1; --q) {
+                        const float inew = fmaxf(M[q] + tr[MI][q], I[q] + tr[II][q]);
+                        M[q] = fmaxf(M[q - 1] + tr[MM_IN][q], I[q - 1] + tr[IM_IN][q]);
+                        I[q] = inew;
+                    }
+                    I[0] = fmaxf(M[0] + tr[MI][0], I[0] + tr[II][0]);
                 }
-                I[0] = fmaxf(M[0] + tr[MI][0], I[0] + tr[II][0]);
                 // pin phase A here, ahead of the polls (left alone, the compiler sinks it past them to its uses
                 // in phase B, and the hop is waited for with nothing to issue)
 #pragma unroll
@@ -287,21 +334,45 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                 // ---- phase B: row i.  Slot 0 reads the previous row's state k0-1 through the lane shift (lane
                 // 0 of a wave w > 0 keeps the left wave's record as the shift's `old`)
                 const float sM = tshift(lastM, xM), sI = tshift(lastI, xI), sD = tshift(D[S - 1], xD);
+                float tmm0, tim0;  // slot 0's entry transitions (LA: from LDS)
+                if constexpr (LA) {
+                    tmm0 = ttab_s[rz + (0 * C2 + 0) * VL + vl].x;
+                    tim0 = ttab_s[rz + (1 * C2 + 0) * VL + vl].x;
+                } else {
+                    tmm0 = tr[MM_IN][0];
+                    tim0 = tr[IM_IN][0];
+                }
+                // DM_IN of chunk c (LA = 2: from LDS, one chunk ahead of use)
+                const float2* tdm_l = ttab_s + rz + 4 * C2 * VL + vl;
+                float2 dmc = LA == 2 ? tdm_l[(C2 - 1) * VL] : make_float2(0.f, 0.f);
+                auto tdm = [&](int q, float2 chunk) -> float {
+                    if constexpr (LA == 2) return (q & 1) ? chunk.y : chunk.x;
+                    else return tr[DM_IN][q];
+                };
                 // the lane's last M first, so it can cross to the next lane for that lane's first D
-                const float mlast = fmaxf(fmaxf(M[S - 1], D[S - 2] + tr[DM_IN][S - 1]), Bt) +
+                const float mlast = fmaxf(fmaxf(M[S - 1], D[S - 2] + tdm(S - 1, dmc)), Bt) +
                                     (((S - 1) & 1) ? ev[(S - 1) / 2].y : ev[(S - 1) / 2].x);
                 float E = mlast;
                 {
                     float pd = sD, mn = tshift(mlast, TNINF), dn = TNINF;
+                    if constexpr (LA == 2) dmc = tdm_l[0];
+                    float2 dmn = dmc;
 #pragma unroll
                     for (int q = 0; q < S; ++q) {
+                        if constexpr (LA == 2) {
+                            if ((q & 1) == 0) {
+                                if (q > 0) dmc = dmn;
+                                if (q / 2 + 1 < C2) dmn = tdm_l[(q / 2 + 1) * VL];
+                                __builtin_amdgcn_sched_barrier(0);
+                            }
+                        }
                         const float od = D[q];
                         float m;
                         if (q == S - 1) {
                             m = mlast;
                         } else {
-                            const float aq = q == 0 ? fmaxf(sM + tr[MM_IN][0], sI + tr[IM_IN][0]) : M[q];
-                            m = fmaxf(fmaxf(aq, pd + tr[DM_IN][q]), Bt) + ((q & 1) ? ev[q / 2].y : ev[q / 2].x);
+                            const float aq = q == 0 ? fmaxf(sM + tmm0, sI + tim0) : M[q];
+                            m = fmaxf(fmaxf(aq, pd + tdm(q, dmc)), Bt) + ((q & 1) ? ev[q / 2].y : ev[q / 2].x);
                             E = fmaxf(E, m);
                         }
                         const float d = q ? fmaxf(mn + tr[MD_IN][q], dn + tr[DD_IN][q]) : mn + tr[MD_IN][0];
@@ -376,18 +447,20 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
 // ------------------------------------------------------------------------------------------------
 // Team variants (vit_kernel.h VitVariant::team = W): appended to vit_variants() by vit_kernel.hip.
 // ------------------------------------------------------------------------------------------------
-#define VIT_TEAM(W_, S_, ELDS_, NT_, PICK_, NAME_)                                                      \
+#define VIT_TEAM_LA(W_, S_, ELDS_, NT_, LA_, PICK_, NAME_)                                              \
     VitVariant{S_,                                                                                     \
-               kTransitions,                                                                           \
+               kTransitions - ((LA_) == 2 ? 5 : (LA_) == 1 ? 4 : 0),                                   \
                ELDS_,                                                                                  \
                false,                                                                                  \
                (NT_) * (W_),                                                                           \
                PICK_,                                                                                  \
-               reinterpret_cast<const void*>(&vit_team_kernel<W_, S_, ELDS_, NT_>),                    \
+               reinterpret_cast<const void*>(&vit_team_kernel<W_, S_, ELDS_, NT_, LA_>),               \
                NAME_,                                                                                  \
                (ELDS_ ? kRows * ((S_) + 1) / 2 * (W_) * kLanes * 8 : 0) +                              \
+                   ((LA_) == 2 ? 5 : (LA_) == 1 ? 4 : 0) * (((S_) + 1) / 2) * (W_) * kLanes * 8 +          \
                    (NT_) * static_cast<int>(sizeof(TeamX<W_>)),                                        \
                W_}
+#define VIT_TEAM(W_, S_, ELDS_, NT_, PICK_, NAME_) VIT_TEAM_LA(W_, S_, ELDS_, NT_, 0, PICK_, NAME_)
 
 const VitVariant* vit_team_variants(int* count) {
     static const VitVariant all[] = {
@@ -403,12 +476,28 @@ const VitVariant* vit_team_variants(int* count) {
         VIT_TEAM(2, 14, true, 4, false, "vit_w2_s14_e"),
         VIT_TEAM(2, 13, false, 4, false, "vit_w2_s13_g"),
         VIT_TEAM(2, 14, false, 4, false, "vit_w2_s14_g"),
-        VIT_TEAM(2, 15, false, 4, true, "vit_w2_s15_g"),
+        VIT_TEAM(2, 15, false, 4, false, "vit_w2_s15_g"),
         VIT_TEAM(2, 16, false, 4, false, "vit_w2_s16_g"),
-        VIT_TEAM(2, 17, false, 4, true, "vit_w2_s17_g"),
-        VIT_TEAM(2, 18, false, 4, true, "vit_w2_s18_g"),
-        VIT_TEAM(2, 19, false, 4, true, "vit_w2_s19_g"),
+        VIT_TEAM(2, 17, false, 4, false, "vit_w2_s17_g"),
+        VIT_TEAM(2, 18, false, 4, false, "vit_w2_s18_g"),
+        VIT_TEAM(2, 19, false, 4, false, "vit_w2_s19_g"),
         VIT_TEAM(3, 13, false, 2, false, "vit_w3_s13_g"),
+        // phase-A transitions in LDS (and DM_IN, `gb`): three waves per SIMD for the two-wave teams up to
+        // S = 19 -- the picks from S = 15 (profiles/r05_team_tune_bands_la.jsonl: 1901.hmm 2.55 vs 2.85 ms,
+        // 2138 / 2207.hmm -3.5 / -5%, cfg5's survivors 21.5 vs 22.6 ms)
+        VIT_TEAM_LA(2, 12, false, 6, 1, false, "vit_w2_s12_ga"),
+        VIT_TEAM_LA(2, 13, false, 6, 1, true, "vit_w2_s13_ga"),
+        VIT_TEAM_LA(2, 14, false, 6, 1, true, "vit_w2_s14_ga"),
+        VIT_TEAM_LA(2, 16, false, 6, 2, false, "vit_w2_s16_gb"),
+        // ... and four waves per SIMD (<= 128 VGPRs, 16-wave workgroups of 8 teams) for the smaller rows
+        VIT_TEAM_LA(2, 11, true, 8, 1, false, "vit_w2_s11_ea4"),
+        VIT_TEAM_LA(2, 11, false, 8, 1, false, "vit_w2_s11_ga4"),
+        VIT_TEAM_LA(2, 11, true, 6, 1, false, "vit_w2_s11_ea"),
+        VIT_TEAM_LA(2, 12, false, 8, 1, false, "vit_w2_s12_ga4"),
+        VIT_TEAM_LA(2, 15, false, 6, 1, true, "vit_w2_s15_ga"),
+        VIT_TEAM_LA(2, 17, false, 6, 2, true, "vit_w2_s17_gb"),
+        VIT_TEAM_LA(2, 18, false, 6, 2, true, "vit_w2_s18_gb"),
+        VIT_TEAM_LA(2, 19, false, 6, 2, true, "vit_w2_s19_gb"),
     };
     *count = static_cast<int>(sizeof(all) / sizeof(all[0]));
     return all;
