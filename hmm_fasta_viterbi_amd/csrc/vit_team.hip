@@ -94,7 +94,7 @@ __device__ __forceinline__ uint64_t u64first(uint64_t x) {
 // MD_IN (the D chain and lazy-F) stay in VGPRs.
 template <int W, int S, bool ELDS, int NT, int LA = 0>
 __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) {
-    static_assert(S >= 2 && W >= 2 && W <= 4, "team shape");
+    static_assert(S >= 2 && W >= 1 && W <= 4, "team shape");  // W = 1: one wave per sequence, no exchange
     constexpr int C2 = (S + 1) / 2;  // float2 chunks per lane (an odd S leaves the last .y unused)
     constexpr int VL = W * kLanes;   // virtual lanes of a team
     constexpr int ROW2 = C2 * VL;    // float2 per table row
@@ -148,7 +148,8 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     // E records of row stamp `st`: publish this wave's E_w (lane 0: one store), and read the other waves'
     // (polling their stamps), returning max_w E_w.
     auto publish_e = [&](float Ew, uint32_t st) {
-        if (lane == 0) lds_write2(&tx.e[st & 1][w], v2f{Ew, __uint_as_float(st)});
+        if constexpr (W > 1)
+            if (lane == 0) lds_write2(&tx.e[st & 1][w], v2f{Ew, __uint_as_float(st)});
     };
     bool hung = false;
     auto wait_e = [&](float Ew, uint32_t st_) -> float {
@@ -186,13 +187,16 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                     a.scores[s] = __uint_as_float(0x7fc00000u);
                     atomicOr(a.errors, msvk::kErrTooLong);
                 }
-                lds_write2(&tx.next[(k + 1) & 1], v2f{__uint_as_float(nteams + tnext), __uint_as_float(k + 1)});
+                if constexpr (W > 1)
+                    lds_write2(&tx.next[(k + 1) & 1], v2f{__uint_as_float(nteams + tnext), __uint_as_float(k + 1)});
             }
-            // one E exchange keeps the team within a sequence of each other (the `next` record's parity)
-            publish_e(TNINF, rc);
-            (void)wait_e(TNINF, rc);
-            ++rc;
-            if (hung) goto fail;
+            if constexpr (W > 1) {
+                // one E exchange keeps the team within a sequence of each other (the `next` record's parity)
+                publish_e(TNINF, rc);
+                (void)wait_e(TNINF, rc);
+                ++rc;
+                if (hung) goto fail;
+            }
         } else {
             const float2 lm = a.lentab[L];
             const float loop = lm.x, move = lm.y;
@@ -253,11 +257,14 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                 uint32_t code = __builtin_amdgcn_readlane(cur, ph);
                 maxcode = code > maxcode ? code : maxcode;
                 code = code < 19u ? code : 19u;
-                float2 ev[C2];  // this row's match scores, requested before the row's independent work
-                {
-                    const float2* er;
-                    if constexpr (ELDS) er = etab_s + code * ROW2 + vl;
-                    else er = a.etab + code * ROW2 + vl;
+                // this row's match scores: from L2, all requested before the row's independent work; from LDS
+                // (ELDS with LA), streamed a chunk ahead in phase B (fewer live VGPRs)
+                constexpr bool EV_STREAM = ELDS && LA;
+                float2 ev[C2];
+                const float2* er;
+                if constexpr (ELDS) er = etab_s + rz + code * ROW2 + vl;
+                else er = a.etab + code * ROW2 + vl;
+                if constexpr (!EV_STREAM) {
 #pragma unroll
                     for (int c = 0; c < C2; ++c) ev[c] = er[c * VL];
                 }
@@ -350,8 +357,10 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                     else return tr[DM_IN][q];
                 };
                 // the lane's last M first, so it can cross to the next lane for that lane's first D
+                if constexpr (EV_STREAM) ev[C2 - 1] = er[(C2 - 1) * VL];
                 const float mlast = fmaxf(fmaxf(M[S - 1], D[S - 2] + tdm(S - 1, dmc)), Bt) +
                                     (((S - 1) & 1) ? ev[(S - 1) / 2].y : ev[(S - 1) / 2].x);
+                if constexpr (EV_STREAM) ev[0] = er[0];
                 float E = mlast;
                 {
                     float pd = sD, mn = tshift(mlast, TNINF), dn = TNINF;
@@ -363,8 +372,13 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                             if ((q & 1) == 0) {
                                 if (q > 0) dmc = dmn;
                                 if (q / 2 + 1 < C2) dmn = tdm_l[(q / 2 + 1) * VL];
-                                __builtin_amdgcn_sched_barrier(0);
                             }
+                        }
+                        if constexpr (EV_STREAM) {
+                            if ((q & 1) == 0 && q / 2 + 1 < C2 - 1) ev[q / 2 + 1] = er[(q / 2 + 1) * VL];
+                        }
+                        if constexpr (LA == 2 || EV_STREAM) {
+                            if ((q & 1) == 0) __builtin_amdgcn_sched_barrier(0);
                         }
                         const float od = D[q];
                         float m;
@@ -392,11 +406,12 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                 lastI = I[S - 1];
                 if (w == 0) {
                     lazy_f(tshift(D[S - 1], TNINF) + tr[DD_IN][0]);
-                    if (lane == 63) lds_write4(&tx.b[rc & 1][0], v4f{lastM, lastI, D[S - 1], __uint_as_float(rc)});
+                    if (W > 1 && lane == 63)
+                        lds_write4(&tx.b[rc & 1][0], v4f{lastM, lastI, D[S - 1], __uint_as_float(rc)});
                 }
                 ++rc;
             }
-            if (leader)  // the team's next sequence (its atomic returned long ago)
+            if (W > 1 && leader)  // the team's next sequence (its atomic returned long ago)
                 lds_write2(&tx.next[(k + 1) & 1], v2f{__uint_as_float(nteams + tnext), __uint_as_float(k + 1)});
             // J(L-1); the score C(L) + tr_move, C == J when tr_E_C == tr_E_J (MSV_HMM.cpp:49-53,112)
             J = fmaxf(J + loop, wait_e(Ew, rc - 1) + tEJ);
@@ -419,7 +434,9 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                 }
             }
         }
-        {
+        if constexpr (W == 1) {
+            item = nteams + __builtin_amdgcn_readfirstlane(tnext);  // (lane 0's atomic)
+        } else {
             v2f r;
             uint32_t spins = 0;
             do {
@@ -494,6 +511,12 @@ const VitVariant* vit_team_variants(int* count) {
         VIT_TEAM_LA(2, 11, false, 8, 1, false, "vit_w2_s11_ga4"),
         VIT_TEAM_LA(2, 11, true, 6, 1, false, "vit_w2_s11_ea"),
         VIT_TEAM_LA(2, 12, false, 8, 1, false, "vit_w2_s12_ga4"),
+        // W = 1 (one wave per sequence, no exchange): the team kernel's row (phase A / B) with the phase-A
+        // transitions (and DM_IN) in LDS, for three waves per SIMD where vit_kernel.hip fits two
+        VIT_TEAM_LA(1, 22, true, 12, 2, false, "vit_w1_s22_eb"),
+        VIT_TEAM_LA(1, 22, true, 12, 1, false, "vit_w1_s22_ea"),
+        VIT_TEAM_LA(1, 22, false, 12, 2, false, "vit_w1_s22_gb"),
+        VIT_TEAM_LA(1, 20, true, 12, 2, false, "vit_w1_s20_eb"),
         VIT_TEAM_LA(2, 15, false, 6, 1, true, "vit_w2_s15_ga"),
         VIT_TEAM_LA(2, 17, false, 6, 2, true, "vit_w2_s17_gb"),
         VIT_TEAM_LA(2, 18, false, 6, 2, true, "vit_w2_s18_gb"),
