@@ -98,6 +98,11 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     constexpr int C2 = (S + 1) / 2;  // float2 chunks per lane (an odd S leaves the last .y unused)
     constexpr int VL = W * kLanes;   // virtual lanes of a team
     constexpr int ROW2 = C2 * VL;    // float2 per table row
+#ifdef VIT_TEAM_TWO_ROWS
+    constexpr bool TWO_ROWS = true;
+#else
+    constexpr bool TWO_ROWS = false;
+#endif
     // transition arrays in LDS: MM_IN, IM_IN, MI, II (LDS slots 0 .. 3), and DM_IN (slot 4, LA = 2)
     constexpr int NLA = LA == 2 ? 5 : LA == 1 ? 4 : 0;
     __shared__ float2 etab_s[ELDS ? kRows * ROW2 : 1];
@@ -248,7 +253,9 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                 }
             };
 
-            for (uint64_t i = 0; i < L; ++i) {
+            // One row.  Rows run two per loop trip where the registers allow it: over two rows the values
+            // return to their registers by themselves (a one-row loop copied some at its back edge).
+            auto row = [&](uint64_t i) -> bool {
                 const uint32_t ph = static_cast<uint32_t>(i) & 63u;
                 if (ph == 0 && i != 0) {
                     cur = nxt;
@@ -333,7 +340,7 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                     // J(i-1) from every wave's E record (the ballot used the same J + loop), N, B
                     const float Jn = J + loop;
                     J = fmaxf(Jn, wait_e(Ew, st) + tEJ);
-                    if (hung) goto fail;
+                    if (hung) return false;
                     N = N + loop;
                     B = fmaxf(N, J) + move;
                 }
@@ -410,7 +417,15 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                         lds_write4(&tx.b[rc & 1][0], v4f{lastM, lastI, D[S - 1], __uint_as_float(rc)});
                 }
                 ++rc;
+                return true;
+            };
+            uint64_t i = 0;
+            if constexpr (TWO_ROWS) {
+                for (; i + 1 < L; i += 2)
+                    if (!row(i) || !row(i + 1)) goto fail;
             }
+            for (; i < L; ++i)
+                if (!row(i)) goto fail;
             if (W > 1 && leader)  // the team's next sequence (its atomic returned long ago)
                 lds_write2(&tx.next[(k + 1) & 1], v2f{__uint_as_float(nteams + tnext), __uint_as_float(k + 1)});
             // J(L-1); the score C(L) + tr_move, C == J when tr_E_C == tr_E_J (MSV_HMM.cpp:49-53,112)
