@@ -103,10 +103,10 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
 #else
     constexpr bool TWO_ROWS = false;
 #endif
-    // transition arrays in LDS: MM_IN, IM_IN, MI, II (LDS slots 0 .. 3), and DM_IN (slot 4, LA = 2)
-    constexpr int NLA = LA == 2 ? 5 : LA == 1 ? 4 : 0;
     __shared__ float2 etab_s[ELDS ? kRows * ROW2 : 1];
-    __shared__ float2 ttab_s[LA ? NLA * C2 * VL : 1];
+    // phase A's pairs as float4 {MM, IM} and {MI, II} per chunk (one ds_read_b128 each), DM_IN as float2
+    __shared__ float4 tpa_s[LA ? 2 * C2 * VL : 1];
+    __shared__ float2 tdm_s[LA == 2 ? C2 * VL : 1];
     __shared__ TeamX<W> tx_s[NT];
     const int lane = threadIdx.x & 63;
     // (readfirstlane: the wave's index is wave-uniform, so branches on it are scalar)
@@ -118,9 +118,13 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     if constexpr (ELDS)
         for (int i = threadIdx.x; i < kRows * ROW2; i += NT * W * 64) etab_s[i] = a.etab[i];
     if constexpr (LA) {
-        constexpr int la_src[5] = {MM_IN, IM_IN, MI, II, DM_IN};
-        for (int i = threadIdx.x; i < NLA * C2 * VL; i += NT * W * 64)
-            ttab_s[i] = a.ttab[la_src[i / (C2 * VL)] * C2 * VL + i % (C2 * VL)];
+        for (int i = threadIdx.x; i < 2 * C2 * VL; i += NT * W * 64) {
+            const int pr = i / (C2 * VL), r = i % (C2 * VL);
+            const float2 x = a.ttab[(pr ? MI : MM_IN) * C2 * VL + r], y = a.ttab[(pr ? II : IM_IN) * C2 * VL + r];
+            tpa_s[i] = make_float4(x.x, x.y, y.x, y.y);
+        }
+        if constexpr (LA == 2)
+            for (int i = threadIdx.x; i < C2 * VL; i += NT * W * 64) tdm_s[i] = a.ttab[DM_IN * C2 * VL + i];
     }
     for (int i = threadIdx.x; i < static_cast<int>(NT * sizeof(TeamX<W>) / 4); i += NT * W * 64)
         reinterpret_cast<uint32_t*>(tx_s)[i] = 0xFFFFFFFFu;  // no stamp matches
@@ -280,10 +284,13 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                 if constexpr (LA) {
                     // chunk by chunk, highest first; each chunk's four pairs read one chunk ahead
                     asm volatile("" : "+v"(rz));
-                    const float2* tl = ttab_s + rz + vl;
+                    const float4* tl = tpa_s + rz + vl;
                     auto ld = [&](int c, float2 (&t)[4]) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) t[j] = tl[(j * C2 + c) * VL];
+                        const float4 p0 = tl[c * VL], p1 = tl[(C2 + c) * VL];
+                        t[0] = make_float2(p0.x, p0.y);
+                        t[1] = make_float2(p0.z, p0.w);
+                        t[2] = make_float2(p1.x, p1.y);
+                        t[3] = make_float2(p1.z, p1.w);
                     };
                     float2 tc[4], tn[4];
                     ld(C2 - 1, tc);
@@ -350,14 +357,15 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                 const float sM = tshift(lastM, xM), sI = tshift(lastI, xI), sD = tshift(D[S - 1], xD);
                 float tmm0, tim0;  // slot 0's entry transitions (LA: from LDS)
                 if constexpr (LA) {
-                    tmm0 = ttab_s[rz + (0 * C2 + 0) * VL + vl].x;
-                    tim0 = ttab_s[rz + (1 * C2 + 0) * VL + vl].x;
+                    const float4 p0 = tpa_s[rz + vl];
+                    tmm0 = p0.x;
+                    tim0 = p0.z;
                 } else {
                     tmm0 = tr[MM_IN][0];
                     tim0 = tr[IM_IN][0];
                 }
                 // DM_IN of chunk c (LA = 2: from LDS, one chunk ahead of use)
-                const float2* tdm_l = ttab_s + rz + 4 * C2 * VL + vl;
+                const float2* tdm_l = tdm_s + rz + vl;
                 float2 dmc = LA == 2 ? tdm_l[(C2 - 1) * VL] : make_float2(0.f, 0.f);
                 auto tdm = [&](int q, float2 chunk) -> float {
                     if constexpr (LA == 2) return (q & 1) ? chunk.y : chunk.x;
