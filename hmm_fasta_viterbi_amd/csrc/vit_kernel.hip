@@ -502,7 +502,7 @@ static const VitVariant* single_wave_variants(int* count) {
         VIT_VARIANT(16, 7, true, false, 8, 0, true, X, "vit_s16_t7a"),
         VIT_VARIANT(18, 7, true, false, 8, 0, true, X, "vit_s18_t7a"),
         VIT_VARIANT(20, 5, true, false, 8, 1, true, P, "vit_s20_t5a"),
-        VIT_VARIANT(22, 5, true, false, 8, 1, true, P, "vit_s22_t5a"),
+        VIT_VARIANT(22, 5, true, false, 8, 1, true, X, "vit_s22_t5a"),
         VIT_VARIANT(22, 0, true, false, 8, 1, true, X, "vit_s22_t0a"),
         VIT_VARIANT(38, 0, false, false, 8, 3, true, X, "vit_s38_t0ga"),
         // one wave per SIMD (4 per workgroup): the 512-register budget holds S = 38 without the 52 spilled

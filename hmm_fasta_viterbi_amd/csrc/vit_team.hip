@@ -106,7 +106,8 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     __shared__ float2 etab_s[ELDS ? kRows * ROW2 : 1];
     // phase A's pairs as float4 {MM, IM} and {MI, II} per chunk (one ds_read_b128 each), DM_IN as float2
     __shared__ float4 tpa_s[LA ? 2 * C2 * VL : 1];
-    __shared__ float2 tdm_s[LA == 2 ? C2 * VL : 1];
+    constexpr int C4 = (C2 + 1) / 2;  // DM_IN chunk pairs (LA = 2): chunks 2p, 2p + 1 as one float4
+    __shared__ float4 tdm_s[LA == 2 ? C4 * VL : 1];
     __shared__ TeamX<W> tx_s[NT];
     const int lane = threadIdx.x & 63;
     // (readfirstlane: the wave's index is wave-uniform, so branches on it are scalar)
@@ -124,7 +125,12 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
             tpa_s[i] = make_float4(x.x, x.y, y.x, y.y);
         }
         if constexpr (LA == 2)
-            for (int i = threadIdx.x; i < C2 * VL; i += NT * W * 64) tdm_s[i] = a.ttab[DM_IN * C2 * VL + i];
+            for (int i = threadIdx.x; i < C4 * VL; i += NT * W * 64) {
+                const int pc = i / VL, l = i % VL;
+                const float2 x = a.ttab[(DM_IN * C2 + 2 * pc) * VL + l];
+                const float2 y = 2 * pc + 1 < C2 ? a.ttab[(DM_IN * C2 + 2 * pc + 1) * VL + l] : make_float2(0.f, 0.f);
+                tdm_s[i] = make_float4(x.x, x.y, y.x, y.y);
+            }
     }
     for (int i = threadIdx.x; i < static_cast<int>(NT * sizeof(TeamX<W>) / 4); i += NT * W * 64)
         reinterpret_cast<uint32_t*>(tx_s)[i] = 0xFFFFFFFFu;  // no stamp matches
@@ -364,12 +370,16 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                     tmm0 = tr[MM_IN][0];
                     tim0 = tr[IM_IN][0];
                 }
-                // DM_IN of chunk c (LA = 2: from LDS, one chunk ahead of use)
-                const float2* tdm_l = tdm_s + rz + vl;
-                float2 dmc = LA == 2 ? tdm_l[(C2 - 1) * VL] : make_float2(0.f, 0.f);
-                auto tdm = [&](int q, float2 chunk) -> float {
-                    if constexpr (LA == 2) return (q & 1) ? chunk.y : chunk.x;
-                    else return tr[DM_IN][q];
+                // DM_IN (LA = 2: from LDS, four slots per ds_read_b128, one pair ahead of use)
+                const float4* tdm_l = tdm_s + rz + vl;
+                float4 dmc = LA == 2 ? tdm_l[((S - 1) / 4) * VL] : make_float4(0.f, 0.f, 0.f, 0.f);
+                auto tdm = [&](int q, float4 p4) -> float {
+                    if constexpr (LA == 2) {
+                        const int r = q & 3;
+                        return r == 0 ? p4.x : r == 1 ? p4.y : r == 2 ? p4.z : p4.w;
+                    } else {
+                        return tr[DM_IN][q];
+                    }
                 };
                 // the lane's last M first, so it can cross to the next lane for that lane's first D
                 if constexpr (EV_STREAM) ev[C2 - 1] = er[(C2 - 1) * VL];
@@ -380,13 +390,13 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                 {
                     float pd = sD, mn = tshift(mlast, TNINF), dn = TNINF;
                     if constexpr (LA == 2) dmc = tdm_l[0];
-                    float2 dmn = dmc;
+                    float4 dmn = dmc;
 #pragma unroll
                     for (int q = 0; q < S; ++q) {
                         if constexpr (LA == 2) {
-                            if ((q & 1) == 0) {
+                            if ((q & 3) == 0) {
                                 if (q > 0) dmc = dmn;
-                                if (q / 2 + 1 < C2) dmn = tdm_l[(q / 2 + 1) * VL];
+                                if (q / 4 + 1 < C4) dmn = tdm_l[(q / 4 + 1) * VL];
                             }
                         }
                         if constexpr (EV_STREAM) {
@@ -537,9 +547,19 @@ const VitVariant* vit_team_variants(int* count) {
         // W = 1 (one wave per sequence, no exchange): the team kernel's row (phase A / B) with the phase-A
         // transitions (and DM_IN) in LDS, for three waves per SIMD where vit_kernel.hip fits two
         VIT_TEAM_LA(1, 22, true, 12, 2, false, "vit_w1_s22_eb"),
-        VIT_TEAM_LA(1, 22, true, 12, 1, false, "vit_w1_s22_ea"),
+        VIT_TEAM_LA(1, 22, true, 12, 1, true, "vit_w1_s22_ea"),
         VIT_TEAM_LA(1, 22, false, 12, 2, false, "vit_w1_s22_gb"),
         VIT_TEAM_LA(1, 20, true, 12, 2, false, "vit_w1_s20_eb"),
+        VIT_TEAM_LA(1, 22, true, 8, 0, false, "vit_w1_s22_e"),
+        VIT_TEAM_LA(1, 22, true, 8, 1, false, "vit_w1_s22_ea2"),
+        VIT_TEAM_LA(1, 20, true, 12, 1, false, "vit_w1_s20_ea"),
+        VIT_TEAM_LA(1, 18, true, 12, 1, false, "vit_w1_s18_ea"),
+        VIT_TEAM_LA(1, 16, true, 12, 1, false, "vit_w1_s16_ea"),
+        VIT_TEAM_LA(1, 14, true, 12, 1, false, "vit_w1_s14_ea"),
+        VIT_TEAM_LA(1, 12, true, 12, 1, false, "vit_w1_s12_ea"),
+        VIT_TEAM_LA(1, 16, true, 16, 1, false, "vit_w1_s16_ea4"),
+        VIT_TEAM_LA(1, 14, true, 16, 1, false, "vit_w1_s14_ea4"),
+        VIT_TEAM_LA(1, 12, true, 16, 1, false, "vit_w1_s12_ea4"),
         VIT_TEAM_LA(2, 15, false, 6, 1, true, "vit_w2_s15_ga"),
         VIT_TEAM_LA(2, 17, false, 6, 2, true, "vit_w2_s17_gb"),
         VIT_TEAM_LA(2, 18, false, 6, 2, true, "vit_w2_s18_gb"),
