@@ -497,7 +497,6 @@ msv_status msv_filter_select_device(int device, const float* d_scores, const uin
     Guard g(device);
     if (!g.ok) return MSV_ERR_NO_DEVICE;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    VIT_HIP(hipMemsetAsync(d_count, 0, sizeof(uint32_t), st));
     return hip_status(
         vitk::launch_select(d_scores, d_offsets, d_order, n, mu, lambda, threshold, d_pvalues, d_selected, d_count, st));
 }

@@ -65,8 +65,8 @@ const VitVariant* vit_team_variants(int* count);  // vit_team.hip
 hipError_t vit_launch(const VitVariant& v, uint32_t blocks, const VitArgs& args, hipStream_t stream,
                       hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 // MSV filter survivors: P-value of every MSV score (msv_pvalue_of, STATS LOCAL MSV), written to pvalues
-// when non-null, and the indices with P <= threshold appended to select (order across waves arbitrary;
-// *count must be zero on entry).
+// when non-null, and the indices with P <= threshold written to select in the order's order (a stable
+// compaction: two launches), their number to *count.
 hipError_t launch_select(const float* scores, const uint64_t* offsets, const uint32_t* order, uint64_t n, float mu,
                          float lambda, double threshold, double* pvalues, uint32_t* select, uint32_t* count,
                          hipStream_t stream);

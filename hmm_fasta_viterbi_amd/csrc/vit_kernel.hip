@@ -403,43 +403,104 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// MSV filter survivors (fused P-value + stream compaction): one thread per sequence, a wave ballot and
-// one atomic per wave.
+// MSV filter survivors: the P-value of every score and a STABLE stream compaction of the sequences with
+// P <= threshold, in the given dequeue order -- two launches of 256 entries per block: (1) P-values and each
+// block's survivor count, (2) each block sums the counts before it and writes its survivors at their exact
+// rank.  With the MSV launch's longest-first order the Viterbi launch then takes its survivors exactly
+// longest first, so its drain tail is its shortest sequences (an unordered append -- one atomic per wave,
+// stretches of 64 in arrival order -- left long survivors in the last round of the persistent grid:
+// cfg3 1.40 vs 1.26 ms, cfg5 21.6 vs 20.0 ms with the team kernels, profiles/r05_select_order.jsonl).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void vit_select_kernel(const float* __restrict__ scores,
-                                                         const uint64_t* __restrict__ offsets,
-                                                         const uint32_t* __restrict__ order, uint64_t n, float mu,
-                                                         float lambda, double threshold, double* __restrict__ pvalues,
-                                                         uint32_t* __restrict__ select, uint32_t* __restrict__ count) {
-    const uint64_t pos = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    bool pass = false;
-    uint64_t i = pos;
-    if (pos < n) {
-        if (order) i = order[pos];  // (a permutation: every sequence is visited once)
-        const double p = msvk::msv_pvalue_of(scores[i], offsets[i + 1] - offsets[i], mu, lambda);
-        if (pvalues) pvalues[i] = p;
-        pass = p <= threshold;
-    }
+namespace {
+constexpr int kSelBlock = 256;
+
+__device__ __forceinline__ bool select_pass(const float* scores, const uint64_t* offsets, const uint32_t* order,
+                                            uint64_t n, float mu, float lambda, double threshold, double* pvalues,
+                                            uint64_t pos, uint32_t* idx) {
+    if (pos >= n) return false;
+    const uint64_t i = order ? order[pos] : pos;  // (a permutation: every sequence is visited once)
+    *idx = static_cast<uint32_t>(i);
+    const double p = msvk::msv_pvalue_of(scores[i], offsets[i + 1] - offsets[i], mu, lambda);
+    if (pvalues) pvalues[i] = p;
+    return p <= threshold;
+}
+
+// Block sum of one uint32 per thread (4 waves).
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* lds4) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) lds4[wv] = v;
+    __syncthreads();
+    const uint32_t t = lds4[0] + lds4[1] + lds4[2] + lds4[3];
+    __syncthreads();
+    return t;
+}
+}  // namespace
+
+__global__ __launch_bounds__(kSelBlock) void vit_select_count_kernel(const float* __restrict__ scores,
+                                                                     const uint64_t* __restrict__ offsets,
+                                                                     const uint32_t* __restrict__ order, uint64_t n,
+                                                                     float mu, float lambda, double threshold,
+                                                                     double* __restrict__ pvalues,
+                                                                     uint32_t* __restrict__ block_counts) {
+    __shared__ uint32_t lds4[4];
+    uint32_t idx = 0;
+    const uint64_t pos = static_cast<uint64_t>(blockIdx.x) * kSelBlock + threadIdx.x;
+    const bool pass = select_pass(scores, offsets, order, n, mu, lambda, threshold, pvalues, pos, &idx);
+    const uint32_t c = block_sum(pass ? 1u : 0u, lds4);
+    if (threadIdx.x == 0) block_counts[blockIdx.x] = c;
+}
+
+__global__ __launch_bounds__(kSelBlock) void vit_select_write_kernel(const float* __restrict__ scores,
+                                                                     const uint64_t* __restrict__ offsets,
+                                                                     const uint32_t* __restrict__ order, uint64_t n,
+                                                                     float mu, float lambda, double threshold,
+                                                                     const uint32_t* __restrict__ block_counts,
+                                                                     uint32_t* __restrict__ select,
+                                                                     uint32_t* __restrict__ count) {
+    __shared__ uint32_t lds4[4];
+    __shared__ uint32_t wave_base[4];
+    // survivors of the blocks before this one
+    uint32_t part = 0;
+    for (uint32_t j = threadIdx.x; j < blockIdx.x; j += kSelBlock) part += block_counts[j];
+    const uint32_t prefix = block_sum(part, lds4);
+    uint32_t idx = 0;
+    const uint64_t pos = static_cast<uint64_t>(blockIdx.x) * kSelBlock + threadIdx.x;
+    const bool pass = select_pass(scores, offsets, order, n, mu, lambda, threshold, nullptr, pos, &idx);
     const uint64_t mask = __builtin_amdgcn_ballot_w64(pass);
-    if (mask == 0) return;
-    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(mask >> 32),
                                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(mask), 0u));
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(count, static_cast<uint32_t>(__popcll(mask)));
-    base = __builtin_amdgcn_readfirstlane(base);
-    if (pass) select[base + below] = static_cast<uint32_t>(i);
+    if (lane == 0) wave_base[wv] = static_cast<uint32_t>(__popcll(mask));
+    __syncthreads();
+    uint32_t base = prefix;
+    for (uint32_t k = 0; k < wv; ++k) base += wave_base[k];
+    if (pass) select[base + below] = idx;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+        *count = prefix + wave_base[0] + wave_base[1] + wave_base[2] + wave_base[3];
 }
 
 hipError_t launch_select(const float* scores, const uint64_t* offsets, const uint32_t* order, uint64_t n, float mu,
                          float lambda, double threshold, double* pvalues, uint32_t* select, uint32_t* count,
                          hipStream_t stream) {
-    const uint64_t blocks = (n + 255) / 256;
+    const uint64_t blocks = (n + kSelBlock - 1) / kSelBlock;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(vit_select_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream, scores, offsets,
-                       order, n, mu, lambda, threshold, pvalues, select, count);
-    return hipGetLastError();
+    if (blocks == 0) return hipMemsetAsync(count, 0, sizeof(uint32_t), stream);
+    // the per-block counts: stream-ordered scratch, so calls on different streams never share it
+    uint32_t* counts = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&counts), blocks * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(vit_select_count_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kSelBlock), 0, stream,
+                       scores, offsets, order, n, mu, lambda, threshold, pvalues, counts);
+    e = hipGetLastError();
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(vit_select_write_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kSelBlock), 0, stream,
+                           scores, offsets, order, n, mu, lambda, threshold, counts, select, count);
+        e = hipGetLastError();
+    }
+    const hipError_t f = hipFreeAsync(counts, stream);
+    return e != hipSuccess ? e : f;
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -299,11 +299,11 @@ msv_status msv_pvalues_device(int device, const float* d_scores, const uint64_t*
                               float lambda, double* d_pvalues, void* stream);
 
 /* MSV filter on the device: the P-value of every score (the formula above, written to d_pvalues when it
- * is not NULL) and the indices of the sequences with P <= threshold appended to d_selected (n uint32 of
- * room), their number in *d_count (one device uint32, zeroed here first).  d_order (NULL or a permutation
- * of 0..n-1, e.g. msv_order_longest_first's) is the order the survivors are listed in, up to the order in
- * which 64-entry stretches of it append (one atomic per stretch): with the longest-first permutation the
- * Viterbi launch dequeues its longest survivors first.  The survivors list feeds
+ * is not NULL) and the indices of the sequences with P <= threshold written to d_selected (n uint32 of
+ * room), their number to *d_count (one device uint32).  d_order (NULL or a permutation of 0..n-1, e.g.
+ * msv_order_longest_first's) is the order the survivors are listed in, exactly (a stable compaction, two
+ * launches): with the longest-first permutation the Viterbi launch dequeues its survivors longest first
+ * and its drain tail is its shortest ones.  The survivors list feeds
  * msv_vit_score_batch_device directly (no host round trip).  `stream` must not be NULL
  * (MSV_ERR_INVALID_ARGUMENT): the profiles' calls take NULL as their own non-blocking stream, which the
  * legacy null stream does not order against, so pass the same explicit stream to the calls it chains. */

@@ -223,8 +223,8 @@ def test_select_list_and_device_count():
 
 def test_filter_select_device_order():
     """msv_filter_select_device: the survivors (P <= F1) equal the host formula's mask, with or without a
-    dequeue order; with msv_order_longest_first's permutation every 64-entry stretch of it appends as one
-    contiguous run in order (one atomic per stretch), so the Viterbi launch takes its longest survivors first."""
+    dequeue order, listed in exactly the order's order (a stable compaction): with msv_order_longest_first's
+    permutation the Viterbi launch takes its survivors longest first."""
     import torch
     from hmm_fasta_viterbi_amd import _native
     prof = "1400.hmm"
@@ -254,16 +254,23 @@ def test_filter_select_device_order():
         got = d_sel[:cnt].cpu().numpy().view(np.uint32).astype(np.int64)
         assert cnt == len(want) and np.array_equal(np.sort(got), want)
         if order is not None:
-            pos = np.empty(n, np.int64)
-            pos[d_ord.cpu().numpy().astype(np.int64)] = np.arange(n)
-            p = pos[got]
-            stretch = p // 64
-            starts = np.r_[True, stretch[1:] != stretch[:-1]]
-            assert len(np.unique(stretch)) == int(starts.sum())  # each stretch one contiguous run ...
-            same = ~starts[1:]
-            assert np.all(p[1:][same] > p[:-1][same])  # ... in the order's order
+            ordv = d_ord.cpu().numpy().astype(np.int64)
+            keep = set(want.tolist())
+            assert np.array_equal(got, np.array([i for i in ordv if i in keep], np.int64))  # exactly the order's order
             lens = np.diff(offsets.astype(np.int64))
-            assert np.all(np.diff(lens[d_ord.cpu().numpy().astype(np.int64)]) <= 0)  # the order is longest first
+            assert np.all(np.diff(lens[got]) <= 0)  # survivors longest first
+            assert np.all(np.diff(lens[ordv]) <= 0)  # the order is longest first
+        else:
+            assert np.array_equal(got, want)  # index order
+    # edge sizes: an empty batch (count 0) and a batch one short of / one past a block of 256
+    for nn in (0, 255, 257):
+        _native.check(L.msv_filter_select_device(0, d_sc.data_ptr(), d_off.data_ptr(), None, nn, m.msv_mu,
+                                                 m.msv_lambda, F1, None, d_sel.data_ptr(), d_cnt.data_ptr(),
+                                                 st.cuda_stream))
+        st.synchronize()
+        cnt = int(d_cnt.item())
+        w = np.nonzero(m.pvalues(sc[:nn], offsets[:nn + 1]) <= F1)[0] if nn else np.zeros(0, np.int64)
+        assert cnt == len(w) and np.array_equal(d_sel[:cnt].cpu().numpy().view(np.uint32).astype(np.int64), w)
 
 
 def test_filter_pipeline_matches_composition():

@@ -33,6 +33,12 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="")
     ap.add_argument("--insert-mode", type=int, default=0)
+    ap.add_argument("--in-place", action="store_true",
+                    help="with --config: keep the WHOLE batch on the device and time each variant on the survivors "
+                         "list msv_filter_select_device makes from the MSV launch's scores (bench.py's viterbi_stage "
+                         "setting: scattered survivor residues, select indirection) instead of a compacted copy")
+    ap.add_argument("--sort-select", action="store_true",
+                    help="with --in-place: re-list the device survivors exactly longest first (host sort, uploaded)")
     ap.add_argument("--longest-first", action="store_true",
                     help="survivors listed longest first (as msv_filter_select_device with the MSV order lists them)")
     a = ap.parse_args()
@@ -55,7 +61,38 @@ def main():
         prof = a.profile
         codes, offsets = random_batch(a.seed, a.n, a.lmin, a.lmax)
     h = msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof))
-    if a.config:  # the survivors of the MSV filter
+    sel_dev = None
+    if a.config and a.in_place:  # bench.py's setting: the survivors selected on the device, in place
+        dev = torch.device("cuda:0")
+        m = msv.MSV_HMM(h)
+        n_all = len(offsets) - 1
+        r_all = torch.from_numpy(codes).to(dev)
+        o_all = torch.from_numpy(offsets.view(np.int64)).to(dev)
+        s_all = torch.empty(n_all, dtype=torch.float32, device=dev)
+        order = torch.empty(n_all, dtype=torch.int32, device=dev)
+        sel = torch.empty(n_all, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        st0 = torch.cuda.Stream(dev)
+        m.reserve_length(int(np.diff(offsets.astype(np.int64)).max()))
+        m.order_longest_first(o_all.data_ptr(), n_all, order.data_ptr(), st0.cuda_stream)
+        m.score_batch_device(r_all.data_ptr(), r_all.numel(), o_all.data_ptr(), n_all, s_all.data_ptr(),
+                             order.data_ptr(), st0.cuda_stream)
+        native.msv_filter_select_device.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_float,
+                                                    C.c_float, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        _native.check(native.msv_filter_select_device(0, s_all.data_ptr(), o_all.data_ptr(), order.data_ptr(), n_all,
+                                                      m.msv_mu, m.msv_lambda, a.F1, None, sel.data_ptr(), cnt.data_ptr(),
+                                                      st0.cuda_stream))
+        torch.cuda.synchronize()
+        k = int(cnt.item())
+        keep = np.sort(sel[:k].cpu().numpy().view(np.uint32).astype(np.int64))
+        if a.sort_select:
+            lens_all = np.diff(offsets.astype(np.int64))
+            srt = keep[np.argsort(-lens_all[keep], kind="stable")].astype(np.uint32)
+            sel[:k].copy_(torch.from_numpy(srt.view(np.int32)))
+            torch.cuda.synchronize()
+        sel_dev = (r_all, o_all, sel, cnt, n_all)
+        cells_res = int(np.diff(offsets.astype(np.int64))[keep].sum())
+    elif a.config:  # the survivors of the MSV filter
         m = msv.MSV_HMM(h)
         sc = m.score_batch(codes=codes, offsets=offsets)
         keep = np.nonzero(m.pvalues(sc, offsets) <= a.F1)[0]
@@ -67,7 +104,7 @@ def main():
         codes, offsets = np.concatenate(parts), offs
     n = len(offsets) - 1
     leng = h.model_length - 1
-    cells = int(offsets[-1]) * leng
+    cells = (cells_res if sel_dev is not None else int(offsets[-1])) * leng
     vit = msv.Viterbi_HMM(h, insert_mode=a.insert_mode)
     import re
 
@@ -79,9 +116,14 @@ def main():
         v for v in vit.variants() if (v.endswith("i") == bool(a.insert_mode)) and states(v) >= leng]
     dev = torch.device("cuda:0")
     st = torch.cuda.Stream(dev)
-    r = torch.from_numpy(codes).to(dev)
-    o = torch.from_numpy(offsets.view(np.int64)).to(dev)
-    s = torch.empty(n, dtype=torch.float32, device=dev)
+    if sel_dev is not None:
+        r, o, d_sel, d_cnt, n = sel_dev
+        sel_ptr, cnt_ptr = d_sel.data_ptr(), d_cnt.data_ptr()
+    else:
+        r = torch.from_numpy(codes).to(dev)
+        o = torch.from_numpy(offsets.view(np.int64)).to(dev)
+        sel_ptr = cnt_ptr = None
+    s = torch.full((n,), float("-inf"), dtype=torch.float32, device=dev)
     vit.reserve_length(int(np.diff(offsets.astype(np.int64)).max()))
     res = {nm: [] for nm in names}
     ref = None
@@ -90,14 +132,16 @@ def main():
         for nm in names:
             vit.set_variant(nm)
             for _ in range(2):
-                vit.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), n, s.data_ptr(), stream=st.cuda_stream)
+                vit.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), n, s.data_ptr(), sel_ptr, cnt_ptr,
+                                       stream=st.cuda_stream)
             evs = []
             for _ in range(a.reps):
                 e0, e1 = C.c_void_p(), C.c_void_p()
                 hip.hipEventCreate(C.byref(e0))
                 hip.hipEventCreate(C.byref(e1))
                 native.msv_vit_debug_time_next_launch(vit._p, e0, e1)
-                vit.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), n, s.data_ptr(), stream=st.cuda_stream)
+                vit.score_batch_device(r.data_ptr(), r.numel(), o.data_ptr(), n, s.data_ptr(), sel_ptr, cnt_ptr,
+                                       stream=st.cuda_stream)
                 evs.append((e0, e1))
             vit.check(st.cuda_stream)
             torch.cuda.synchronize()
@@ -117,6 +161,7 @@ def main():
         vit.set_variant(nm)
         info = vit.describe()
         print(json.dumps({"profile": prof, "config": a.config or None, "longest_first": a.longest_first,
+                          "in_place": a.in_place, "sort_select": a.sort_select,
                           "sequences": n, "residues": int(offsets[-1]),
                           "variant": nm, "ms_med": round(ms, 4), "ms_min": round(min(res[nm]), 4),
                           "gcups": round(cells / (ms * 1e-3) / 1e9, 1),
