@@ -60,7 +60,9 @@ def main():
     else:
         prof = a.profile
         codes, offsets = random_batch(a.seed, a.n, a.lmin, a.lmax)
-    h = msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof))
+        if a.longest_first:  # the same residues re-cut with the lengths in descending order
+            offsets[1:] = np.cumsum(np.sort(np.diff(offsets.astype(np.int64)))[::-1]).astype(np.uint64)
+    h =msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof))
     sel_dev = None
     if a.config and a.in_place:  # bench.py's setting: the survivors selected on the device, in place
         dev = torch.device("cuda:0")
