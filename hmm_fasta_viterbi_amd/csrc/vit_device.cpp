@@ -115,6 +115,7 @@ struct msv_vit_profile {
     uint32_t* d_ord = nullptr;
     size_t ord_cap = 0;
     hipEvent_t time_start = nullptr, time_stop = nullptr;  // msv_vit_debug_time_next_launch
+    uint64_t* d_stamps = nullptr;                          // msv_vit_debug_set_stamps (tools only)
 };
 
 namespace {
@@ -238,6 +239,7 @@ msv_status launch(msv_vit_profile* p, const uint8_t* d_residues, const uint64_t*
     a.tr_B_Mk = p->tr_B_Mk;
     a.tr_E_C = p->tr_E_C;
     a.tr_E_J = p->tr_E_J;
+    a.stamps = p->d_stamps;
     // one wave (team) per sequence: no more workgroups than the items need (a device count is bounded by n)
     const uint64_t per_block = static_cast<uint64_t>(p->v->sequences_per_block());
     const uint64_t need = (n + per_block - 1) / per_block;
@@ -448,6 +450,14 @@ msv_status msv_vit_debug_time_next_launch(msv_vit_profile* p, void* start, void*
     if (!p) return MSV_ERR_INVALID_ARGUMENT;
     p->time_start = static_cast<hipEvent_t>(start);
     p->time_stop = static_cast<hipEvent_t>(stop);
+    return MSV_OK;
+}
+
+// Diagnostic (tools/vit_timeline.py, not in msv.h): subsequent team-kernel launches write their timeline to
+// d_stamps (4 uint64 per list entry, then 4 per wave; the caller sizes it), nullptr turns it off.
+msv_status msv_vit_debug_set_stamps(msv_vit_profile* p, uint64_t* d_stamps) {
+    if (!p) return MSV_ERR_INVALID_ARGUMENT;
+    p->d_stamps = d_stamps;
     return MSV_OK;
 }
 

@@ -34,6 +34,9 @@ struct VitArgs {
     uint64_t n;
     uint32_t lentab_n;
     float tr_B_Mk, tr_E_C, tr_E_J;
+    // diagnostic timeline (tools/vit_timeline.py; nullptr in production, team kernels only): per list entry j
+    // {realtime start, end, hw id << 32 | wave, length}, then per wave {entry, tables staged, exit, XCC id}
+    uint64_t* stamps;
 };
 
 // One compiled instantiation: S states per lane (G = 64 lanes per sequence, covers 64 * S states), the first

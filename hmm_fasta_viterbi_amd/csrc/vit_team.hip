@@ -109,6 +109,7 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     constexpr int C4 = (C2 + 1) / 2;  // DM_IN chunk pairs (LA = 2): chunks 2p, 2p + 1 as one float4
     __shared__ float4 tdm_s[LA == 2 ? C4 * VL : 1];
     __shared__ TeamX<W> tx_s[NT];
+    const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();  // (a.stamps only)
     const int lane = threadIdx.x & 63;
     // (readfirstlane: the wave's index is wave-uniform, so branches on it are scalar)
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -135,6 +136,7 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     for (int i = threadIdx.x; i < static_cast<int>(NT * sizeof(TeamX<W>) / 4); i += NT * W * 64)
         reinterpret_cast<uint32_t*>(tx_s)[i] = 0xFFFFFFFFu;  // no stamp matches
     __syncthreads();
+    const uint64_t t_staged = __builtin_amdgcn_s_memrealtime();
 
     float tr[kTransitions][S];
 #pragma unroll
@@ -186,13 +188,24 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
 
     while (item < total) {
         uint32_t tnext = 0;
-        if (leader) tnext = atomicAdd(a.counter, 1u);  // the team's next sequence, published at this one's end
+        // The team's next sequence.  Teams (W > 1) take it once this sequence's first row has run: at the
+        // launch's start every team's atomic hits the one counter at once, and taken first it would sit ahead
+        // of the residue loads the first row waits for (cfg5 -1.4%, profiles/r05_ab_vit_take_late.jsonl); a
+        // single wave (W = 1) takes it first (late was +0.7% on cfg3).
+        bool taken = false;
+        auto take = [&]() {
+            taken = true;
+            if (leader) tnext = atomicAdd(a.counter, 1u);
+        };
+        if constexpr (W == 1) take();
         // (readfirstlane: the sequence, its bounds and so every branch on them are wave-uniform -- scalar
         // branches and a scalar row counter, not exec-masked regions)
         const uint32_t s = __builtin_amdgcn_readfirstlane(a.select ? a.select[item] : item);
+        const uint64_t t_seq = __builtin_amdgcn_s_memrealtime();
         const uint64_t o0 = u64first(a.offsets[s < a.n ? s : 0]);
         const uint64_t L = s < a.n ? u64first(a.offsets[s + 1]) - o0 : 0;
         if (s >= a.n || L == 0 || L >= a.lentab_n) {
+            if (!taken) take();
             if (leader) {
                 if (s >= a.n) {
                     atomicOr(a.errors, msvk::kErrBadOrder);  // a survivors entry outside the batch: skipped
@@ -271,6 +284,9 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                     cur = nxt;
                     nxt = (i + 64 + lane < L) ? res[i + 64 + lane] : 0u;
                 }
+
+                if constexpr (W > 1)
+                    if (i == 1) take();
                 uint32_t code = __builtin_amdgcn_readlane(cur, ph);
                 maxcode = code > maxcode ? code : maxcode;
                 code = code < 19u ? code : 19u;
@@ -444,6 +460,7 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
             }
             for (; i < L; ++i)
                 if (!row(i)) goto fail;
+            if (!taken) take();  // (W > 1: a one-row sequence)
             if (W > 1 && leader)  // the team's next sequence (its atomic returned long ago)
                 lds_write2(&tx.next[(k + 1) & 1], v2f{__uint_as_float(nteams + tnext), __uint_as_float(k + 1)});
             // J(L-1); the score C(L) + tr_move, C == J when tr_E_C == tr_E_J (MSV_HMM.cpp:49-53,112)
@@ -465,6 +482,15 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                 } else {
                     a.scores[s] = sc;
                 }
+                if (a.stamps) {  // diagnostic timeline (nullptr in production)
+                    uint32_t hwid = 0;
+                    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+                    uint64_t* st = a.stamps + 4 * static_cast<uint64_t>(item);
+                    st[0] = t_seq;
+                    st[1] = __builtin_amdgcn_s_memrealtime();
+                    st[2] = (static_cast<uint64_t>(hwid) << 32) | (blockIdx.x * NT * W + wv);
+                    st[3] = L;
+                }
             }
         }
         if constexpr (W == 1) {
@@ -483,6 +509,15 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     if (false) {
     fail:
         if (lane == 0) atomicOr(a.errors, msvk::kErrTeamHang);
+    }
+    if (a.stamps && lane == 0) {  // diagnostic: this wave's entry, tables staged, exit, XCC id
+        uint32_t xcc = 0;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        uint64_t* st = a.stamps + 4 * (total + blockIdx.x * NT * W + wv);
+        st[0] = t_entry;
+        st[1] = t_staged;
+        st[2] = __builtin_amdgcn_s_memrealtime();
+        st[3] = xcc;
     }
     // the last wave to finish resets the slot's counters for its next launch
     if (lane == 0) {
