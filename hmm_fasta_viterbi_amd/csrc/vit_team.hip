@@ -567,6 +567,10 @@ const VitVariant* vit_team_variants(int* count) {
         VIT_TEAM(2, 18, false, 4, false, "vit_w2_s18_g"),
         VIT_TEAM(2, 19, false, 4, false, "vit_w2_s19_g"),
         VIT_TEAM(3, 13, false, 2, false, "vit_w3_s13_g"),
+        // one- / two-team workgroups (tail companions: small enough to start on a CU as another launch's
+        // waves leave it)
+        VIT_TEAM(2, 11, false, 1, false, "vit_w2_s11_g1"),
+        VIT_TEAM(2, 11, false, 2, false, "vit_w2_s11_g2"),
         // phase-A transitions in LDS (and DM_IN, `gb`): three waves per SIMD for the two-wave teams up to
         // S = 19 -- the picks from S = 15 (profiles/r05_team_tune_bands_la.jsonl: 1901.hmm 2.55 vs 2.85 ms,
         // 2138 / 2207.hmm -3.5 / -5%, cfg5's survivors 21.5 vs 22.6 ms)
