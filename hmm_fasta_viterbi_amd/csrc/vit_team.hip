@@ -368,7 +368,17 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                     }
                     // J(i-1) from every wave's E record (the ballot used the same J + loop), N, B
                     const float Jn = J + loop;
+#ifdef VIT_AB_NO_CHAIN
+                    // timing-only A/B build (wrong scores): J no longer waits for the row's E, so the B -> cells
+                    // -> E -> J -> B chain is cut -- bounds what taking E off the chain can gain
+                    {
+                        const float sink = wait_e(Ew, st) + tEJ;
+                        asm volatile("" ::"v"(sink));
+                        J = Jn;
+                    }
+#else
                     J = fmaxf(Jn, wait_e(Ew, st) + tEJ);
+#endif
                     if (hung) return false;
                     N = N + loop;
                     B = fmaxf(N, J) + move;
