@@ -369,19 +369,21 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                     // J(i-1) from every wave's E record (the ballot used the same J + loop), N, B
                     const float Jn = J + loop;
 #ifdef VIT_AB_NO_CHAIN
-                    // timing-only A/B build (wrong scores): J no longer waits for the row's E, so the B -> cells
-                    // -> E -> J -> B chain is cut -- bounds what taking E off the chain can gain
-                    {
-                        const float sink = wait_e(Ew, st) + tEJ;
-                        asm volatile("" ::"v"(sink));
-                        J = Jn;
-                    }
+                    // timing-only A/B build (scores differ on rows where J rises): B from the J of one row
+                    // earlier, so the row's B no longer waits for its E (the B -> cells -> E -> J -> B chain gets
+                    // a row of slack) while J, and so the E ballot's rare path, stay as they are -- bounds what
+                    // taking E off the chain can gain
+                    const float Jold = J;
+                    J = fmaxf(Jn, wait_e(Ew, st) + tEJ);
+                    if (hung) return false;
+                    N = N + loop;
+                    B = fmaxf(N, Jold + loop) + move;
 #else
                     J = fmaxf(Jn, wait_e(Ew, st) + tEJ);
-#endif
                     if (hung) return false;
                     N = N + loop;
                     B = fmaxf(N, J) + move;
+#endif
                 }
                 const float Bt = B + tBM;
                 // ---- phase B: row i.  Slot 0 reads the previous row's state k0-1 through the lane shift (lane

@@ -431,3 +431,47 @@ def test_team_variant_stress(name):
             assert np.array_equal(bits(score_custom(p, codes, offsets)), bits(want)), (name, prof, consts)
         finally:
             _native.lib().msv_vit_profile_destroy(p)
+
+
+@pytest.mark.parametrize("name", ["vit_w1_s22_ea", "vit_w2_s11_g"])
+def test_timeline_stamps_leave_scores_unchanged(name):
+    """The diagnostic timeline (msv_vit_debug_set_stamps, tools/vit_timeline.py): a stamped launch scores
+    bitwise as an unstamped one, every list entry gets one record (start <= end, its own length) and every
+    wave its {entry <= tables staged <= exit}; nullptr turns it off again."""
+    import ctypes as C
+    import torch
+    from hmm_fasta_viterbi_amd import _native
+    lib = _native.lib()
+    lib.msv_vit_debug_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
+    prof = "1400.hmm"
+    e = vit(prof)
+    e.set_variant(name)
+    info = e.describe()
+    nw = info["blocks"] * info["waves_per_block"]
+    codes, offsets = mixed_batch(prof, 77, 60, 1, 500)
+    n = len(offsets) - 1
+    dev = torch.device("cuda:0")
+    d_res = torch.from_numpy(codes).to(dev)
+    d_off = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    plain = torch.empty(n, dtype=torch.float32, device=dev)
+    stamped = torch.empty(n, dtype=torch.float32, device=dev)
+    stamps = torch.zeros((n + nw) * 4, dtype=torch.int64, device=dev)
+    st = torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    e.score_batch_device(d_res.data_ptr(), codes.size, d_off.data_ptr(), n, plain.data_ptr(), None, None,
+                         st.cuda_stream)
+    assert lib.msv_vit_debug_set_stamps(e._p, stamps.data_ptr()) == 0
+    e.score_batch_device(d_res.data_ptr(), codes.size, d_off.data_ptr(), n, stamped.data_ptr(), None, None,
+                         st.cuda_stream)
+    assert lib.msv_vit_debug_set_stamps(e._p, None) == 0
+    st.synchronize()
+    e.check(st.cuda_stream)
+    assert np.array_equal(bits(plain.cpu().numpy()), bits(stamped.cpu().numpy()))
+    x = stamps.cpu().numpy().view(np.uint64).reshape(n + nw, 4)
+    lens = np.diff(offsets.astype(np.int64))
+    live = lens > 0  # (empty sequences are scored without a record)
+    seq = x[:n][live]
+    assert np.all(seq[:, 0] > 0) and np.all(seq[:, 0] <= seq[:, 1])
+    assert np.array_equal(seq[:, 3].astype(np.int64), lens[live])
+    used = x[n:][x[n:, 2] > 0]
+    assert len(used) >= 1 and np.all(used[:, 0] <= used[:, 1]) and np.all(used[:, 1] <= used[:, 2])
