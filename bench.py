@@ -182,6 +182,7 @@ def cpu_baseline(profile_path, codes, offsets, gpu_scores, target_s, threads):
     }
 
 
+VIT_WARMUP = 20  # untimed Viterbi launches before the timed ones
 VIT_OPS_PER_CELL = 14  # fp32 ops per Viterbi DP cell (msv.h): M 3 adds + 3 max + 1 add, I 2 + 1, D 2 + 1, E 1
 
 
@@ -218,10 +219,12 @@ def viterbi_stage(args, msv_engine, prof_path, dev, stream, d_res, residues, d_o
         vit.score_batch_device(d_res.data_ptr(), residues, d_off.data_ptr(), n, d_vsc.data_ptr(), d_sel.data_ptr(),
                                d_cnt.data_ptr(), sh)
 
-    for _ in range(3):
+    # warm until the launches are steady: after the MSV phase the first Viterbi launches run slower (cfg3:
+    # 1.47 ms falling to 1.35 ms over ten launches behind three warm-ups, profiles/r05_bench_cfg3_vit_warmup.json)
+    for _ in range(VIT_WARMUP):
         launch()
     torch.cuda.synchronize(dev)
-    steps = max(3, args.steps // 2)
+    steps = max(10, args.steps)
     events = [(hip_event(), hip_event()) for _ in range(steps)]
     t0 = time.perf_counter()
     for ev in events:
@@ -298,7 +301,7 @@ def viterbi_stage(args, msv_engine, prof_path, dev, stream, d_res, residues, d_o
         "kernel_variant": info["variant"],
         "kernel_ms": round(kms, 4),
         "kernel_ms_launches": [round(x, 4) for x in kall],
-        "kernel_ms_note": "median over the timed launches (each timed by HIP events the launch itself updates)",
+        "kernel_ms_note": f"median over the timed launches (each timed by HIP events the launch itself updates), after {VIT_WARMUP} untimed ones",
         "ms_per_launch_wall": round(wall_ms, 4),
         "M_residues_s": round(surv_res / (kms * 1e-3) / 1e6, 2),
         "gcups": round(cells / (kms * 1e-3) / 1e9, 2),

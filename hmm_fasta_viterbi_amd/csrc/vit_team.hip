@@ -49,7 +49,10 @@ namespace vitk {
 namespace {
 
 constexpr float TNINF = -__builtin_inff();
-constexpr int kTeamEarlyD = 8;  // slots of the unconditional first lazy-F pass (vit_kernel.hip kEarlyD)
+#ifndef VIT_TEAM_EARLY_D
+#define VIT_TEAM_EARLY_D 8
+#endif
+constexpr int kTeamEarlyD = VIT_TEAM_EARLY_D;  // slots of the unconditional first lazy-F pass (vit_kernel.hip kEarlyD)
 constexpr int DPP_WSHR1 = 0x138;
 // A poll that spins this long means the team's protocol broke (a bug, never data): the wave latches
 // kErrTeamHang and leaves the kernel instead of holding the GPU (each poll is one LDS round trip, so this is
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                         cand = tshift(D[S - 1], TNINF) + tr[DD_IN][0];
                     }
                 };
-                if constexpr (S > kTeamEarlyD) {
+                if constexpr (kTeamEarlyD > 0 && S > kTeamEarlyD) {
                     // the first pass over slots 0 .. kTeamEarlyD-1 unconditionally, the rest only if some lane
                     // would still change (vit_kernel.hip: a slot that changes nowhere ends the chain)
                     D[0] = fmaxf(D[0], cand);
