@@ -25,7 +25,7 @@ namespace {
 
 constexpr uint32_t kDefaultMaxLength = 131072;
 constexpr float kNinf = -std::numeric_limits<float>::infinity();
-// d_words: [2k, 2k+1] = launch slot k's dequeue counters {next index, waves left} (zero between launches),
+// d_words: [2k, 2k+1] = launch slot k's dequeue counters {next index, leavers} (zero between launches),
 // [kErrWord] = sticky error bits of device launches (msv_vit_profile_check), [kHostErrWord] = the error bits
 // of the synchronous host calls, which report and clear only their own, [kSelWord] = msv_vit_filter_batch's
 // survivors count.

@@ -29,7 +29,7 @@ struct VitArgs {
     const uint32_t* select_count;  // optional device count of `select` entries (else n)
     const float2* lentab;       // [lentab_n] {tr_loop, tr_move} by length (host logf)
     float* scores;              // written at the sequence index
-    uint32_t* counter;          // {dequeue head, finished waves}: zero on entry, zero again on exit
+    uint32_t* counter;          // {dequeue head, leavers: workgroups (vit_kernel) / waves (team)}: zero on entry and exit
     uint32_t* errors;           // sticky error bits (msvk::kErrBadResidue / kErrTooLong)
     uint64_t n;
     uint32_t lentab_n;

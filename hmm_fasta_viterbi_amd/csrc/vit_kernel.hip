@@ -93,6 +93,7 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
     constexpr int ND = NTL - NM;                          // ... by the D pass
     __shared__ float2 etab_s[ELDS ? kRows * ROW2 : 1];
     __shared__ float2 ttab_s[NTL ? NTL * ROW2 : 1];
+    __shared__ uint32_t exited_s;  // waves of this workgroup that have left (the exit count below)
     const int lane = threadIdx.x & 63;
     // (readfirstlane: wave-uniform, so the sequence, its bounds and every branch on them are scalar)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -101,7 +102,8 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
         for (int i = threadIdx.x; i < kRows * ROW2; i += WAVES * 64) etab_s[i] = a.etab[i];
     if constexpr (NTL > 0)
         for (int i = threadIdx.x; i < NTL * ROW2; i += WAVES * 64) ttab_s[i] = a.ttab[NTREG * ROW2 + i];
-    if constexpr (ELDS || NTL > 0) __syncthreads();
+    if (threadIdx.x == 0) exited_s = 0;
+    __syncthreads();
 
     // transition arrays 0 .. NTREG-1 live in VGPRs for the whole launch, NTREG .. 6 in LDS (re-read every row)
     float tr[NTREG ? NTREG : 1][S];
@@ -392,10 +394,14 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
         if (lane == 0) t = atomicAdd(a.counter, 1u);
         item = nwaves + __builtin_amdgcn_readfirstlane(t);
     }
-    // the last wave to finish resets the counters for the next launch on this profile
+    // the last workgroup to finish resets the counters for the next launch on this profile.  One grid-level
+    // atomic per workgroup (by its last wave, counted in LDS), not per wave: a device-count launch of few
+    // survivors runs thousands of waves that find no work, and their same-address exit atomics delayed the
+    // launch's end (cfg2 in place, 8,192 waves for 260 survivors: 0.223 -> 0.206 ms,
+    // profiles/r05_ab_wg_exit.jsonl; the MSV and team kernels were neutral / +1.3% and keep a count per wave)
     if (lane == 0) {
         __threadfence();
-        if (atomicAdd(a.counter + 1, 1u) == nwaves - 1) {
+        if (atomicAdd(&exited_s, 1u) == WAVES - 1 && atomicAdd(a.counter + 1, 1u) == gridDim.x - 1) {
             atomicExch(a.counter, 0u);
             atomicExch(a.counter + 1, 0u);
         }

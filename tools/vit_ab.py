@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--profile", default="1400.hmm")
     ap.add_argument("--lmin", type=int, default=300)
     ap.add_argument("--lmax", type=int, default=500)
+    ap.add_argument("--in-place", action="store_true", help="bench.py's setting (vit_tune.py --in-place)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     for r in range(a.rounds):
@@ -28,8 +29,9 @@ def main():
             env = dict(os.environ, MSV_LIB_PATH=os.path.abspath(lib))
             batch = (["--profile", a.profile, "--n", str(a.n), "--lmin", str(a.lmin), "--lmax", str(a.lmax)] if a.n
                      else ["--config", a.config])
-            out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "vit_tune.py"), *batch,
-                                  "--longest-first", "--rounds", "1", "--reps", "5", "--variants", a.variant],
+            order = ["--in-place"] if a.in_place else ["--longest-first"]
+            out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "vit_tune.py"), *batch, *order,
+                                  "--rounds", "1", "--reps", "5", "--variants", a.variant],
                                  env=env, capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
                 sys.exit(out.stderr[-2000:])
