@@ -97,6 +97,17 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
     const int lane = threadIdx.x & 63;
     // (readfirstlane: wave-uniform, so the sequence, its bounds and every branch on them are scalar)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t total = a.select_count ? static_cast<uint64_t>(*a.select_count) : a.n;
+    if (static_cast<uint64_t>(blockIdx.x) * WAVES >= total) {
+        // no sequence for this workgroup (a device-count launch is sized for n, the count may be far less:
+        // cfg2's 260 survivors of 10,000): no first item, and none of the queue's (it starts at the grid's
+        // wave count) -- leave without staging the tables, counted like any other workgroup
+        if (threadIdx.x == 0 && atomicAdd(a.counter + 1, 1u) == gridDim.x - 1) {
+            atomicExch(a.counter, 0u);
+            atomicExch(a.counter + 1, 0u);
+        }
+        return;
+    }
 
     if constexpr (ELDS)
         for (int i = threadIdx.x; i < kRows * ROW2; i += WAVES * 64) etab_s[i] = a.etab[i];
@@ -130,7 +141,6 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
         }
     };
 
-    const uint64_t total = a.select_count ? static_cast<uint64_t>(*a.select_count) : a.n;
     const uint32_t nwaves = gridDim.x * WAVES;
     uint32_t item = blockIdx.x * WAVES + wave;
     while (item < total) {
