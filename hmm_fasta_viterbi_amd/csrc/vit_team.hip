@@ -113,6 +113,16 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     __shared__ float4 tdm_s[LA == 2 ? C4 * VL : 1];
     __shared__ TeamX<W> tx_s[NT];
     const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();  // (a.stamps only)
+    const uint64_t total = a.select_count ? static_cast<uint64_t>(*a.select_count) : a.n;
+    if (static_cast<uint64_t>(blockIdx.x) * NT >= total) {
+        // no sequence for this workgroup (vit_kernel.hip: a device-count launch sized for n): leave at once,
+        // counted as its NT * W waves
+        if (threadIdx.x == 0 && atomicAdd(a.counter + 1, static_cast<uint32_t>(NT * W)) == (gridDim.x - 1) * NT * W) {
+            atomicExch(a.counter, 0u);
+            atomicExch(a.counter + 1, 0u);
+        }
+        return;
+    }
     const int lane = threadIdx.x & 63;
     // (readfirstlane: the wave's index is wave-uniform, so branches on it are scalar)
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -157,7 +167,6 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     // the phase-A arrays out of the row loop into VGPRs (which would undo them)
     uint32_t rz = 0;
 
-    const uint64_t total = a.select_count ? static_cast<uint64_t>(*a.select_count) : a.n;
     const uint32_t nteams = gridDim.x * NT;
     uint32_t item = blockIdx.x * NT + team;  // first sequence static
     uint32_t k = 0;                          // the team's sequence ordinal
