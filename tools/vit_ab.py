@@ -22,13 +22,14 @@ def main():
     ap.add_argument("--lmin", type=int, default=300)
     ap.add_argument("--lmax", type=int, default=500)
     ap.add_argument("--in-place", action="store_true", help="bench.py's setting (vit_tune.py --in-place)")
+    ap.add_argument("--config-n", type=int, default=0, help="the config's first N sequences (vit_tune.py)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     for r in range(a.rounds):
         for lib in a.libs:
             env = dict(os.environ, MSV_LIB_PATH=os.path.abspath(lib))
             batch = (["--profile", a.profile, "--n", str(a.n), "--lmin", str(a.lmin), "--lmax", str(a.lmax)] if a.n
-                     else ["--config", a.config])
+                     else ["--config", a.config] + (["--config-n", str(a.config_n)] if a.config_n else []))
             order = ["--in-place"] if a.in_place else ["--longest-first"]
             out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "vit_tune.py"), *batch, *order,
                                   "--rounds", "1", "--reps", "5", "--variants", a.variant],

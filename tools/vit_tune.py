@@ -37,6 +37,7 @@ def main():
                     help="with --config: keep the WHOLE batch on the device and time each variant on the survivors "
                          "list msv_filter_select_device makes from the MSV launch's scores (bench.py's viterbi_stage "
                          "setting: scattered survivor residues, select indirection) instead of a compacted copy")
+    ap.add_argument("--config-n", type=int, default=0, help="with --config: that config's first N sequences only")
     ap.add_argument("--sort-select", action="store_true",
                     help="with --in-place: re-list the device survivors exactly longest first (host sort, uploaded)")
     ap.add_argument("--longest-first", action="store_true",
@@ -57,12 +58,15 @@ def main():
     if a.config:
         prof, n, lmin, lmax, seed, scaling = CONFIGS[a.config]
         codes, offsets = random_batch(seed * 1000 if scaling == "weak" else seed, n, lmin, lmax)
+        if a.config_n:
+            offsets = offsets[:a.config_n + 1].copy()
+            codes = codes[:int(offsets[-1])]
     else:
         prof = a.profile
         codes, offsets = random_batch(a.seed, a.n, a.lmin, a.lmax)
         if a.longest_first:  # the same residues re-cut with the lengths in descending order
             offsets[1:] = np.cumsum(np.sort(np.diff(offsets.astype(np.int64)))[::-1]).astype(np.uint64)
-    h =msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof))
+    h = msv.Profile_HMM(os.path.join(ROOT, "data", "profile_HMMs", prof))
     sel_dev = None
     if a.config and a.in_place:  # bench.py's setting: the survivors selected on the device, in place
         dev = torch.device("cuda:0")
