@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "msv_kernel_impl.h"
@@ -45,6 +46,11 @@ namespace {
 
 constexpr float NINF = -__builtin_inff();
 constexpr int kEarlyD = 8;  // slots of the unconditional first lazy-F pass before its early-exit test
+#ifndef VIT_EARLY_HOP_STATES
+#define VIT_EARLY_HOP_STATES 8
+#endif
+// rows of S < kEarlyD: states (over whole-lane hops) of the unconditional first lazy-F passes
+constexpr int kEarlyHopStates = VIT_EARLY_HOP_STATES;
 
 __device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 __device__ __forceinline__ uint64_t u64first(uint64_t x) {
@@ -88,6 +94,7 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
     constexpr bool TWO_ROWS = S <= 24;
     constexpr int C2 = S / 2;
     constexpr int ROW2 = C2 * kLanes;                     // float2 per table row
+    constexpr int kEarlyHops = S < kEarlyD ? kEarlyHopStates / S : 0;
     constexpr int NTL = kTransitions - NTREG;             // transition arrays in LDS
     constexpr int NM = NTREG >= MD_IN ? 0 : MD_IN - NTREG;  // ... of them used by the M/I pass
     constexpr int ND = NTL - NM;                          // ... by the D pass
@@ -142,6 +149,7 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
     };
 
     const uint32_t nwaves = gridDim.x * WAVES;
+    const bool few = total <= nwaves;  // wave-uniform: a latency-bound launch (no wave takes a second sequence)
     uint32_t item = blockIdx.x * WAVES + wave;
     while (item < total) {
         const uint32_t s = __builtin_amdgcn_readfirstlane(a.select ? a.select[item] : item);
@@ -177,7 +185,7 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
             // than the old ones (the old M(k) is read after the new one is made), so a one-row loop copied
             // the whole row back at its back edge (22 v_mov per row at S = 22); over two rows the values
             // return to their registers by themselves.
-            auto row = [&](uint64_t i) {
+            auto row = [&](uint64_t i, auto hops_c) {  // hops_c: std::bool_constant, the short-row hops
                 const uint32_t ph = static_cast<uint32_t>(i) & 63u;
                 if (ph == 0 && i != 0) {
                     cur = nxt;
@@ -367,6 +375,23 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                         cand = sDn + tdd(0);
                         if (wave_any(cand > D[0])) lazy_f();
                     }
+                } else if constexpr (kEarlyHops > 1 && decltype(hops_c)::value) {
+                    // short rows of a latency-bound launch (at most one sequence per wave): the same first kEarlyD
+                    // states of the chain as above, here over kEarlyHops lanes -- whole-lane passes with their
+                    // lane shifts run unconditionally (a D path crossing lanes costs a ballot and a branch per hop
+                    // on the row's chain otherwise), then the ballot once.  cfg2's survivors -6.5%, 200.hmm x 300
+                    // -13%; with several sequences per wave the extra passes cost issue slots the other waves
+                    // would use (100.hmm x 20k +11% with hops), so those launches keep the ballot first -- at
+                    // +2-3% for the second copy of the row loop (profiles/r05_ab_vit_short_row_hops.jsonl)
+#pragma unroll
+                    for (int h = 0; h < kEarlyHops; ++h) {
+                        D[0] = fmaxf(D[0], cand);
+#pragma unroll
+                        for (int q = 1; q < S; ++q) D[q] = fmaxf(D[q], D[q - 1] + tdd(q));
+                        sDn = shift64(D[S - 1], sDn);
+                        cand = sDn + tdd(0);
+                    }
+                    if (wave_any(cand > D[0])) lazy_f();
                 } else {
                     if (__builtin_expect(wave_any(cand > D[0]), 0)) lazy_f();
                 }
@@ -383,13 +408,23 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                 B = fmaxf(N, J) + move;
             };
             uint64_t i = 0;
-            if constexpr (TWO_ROWS) {
-                for (; i + 1 < L; i += 2) {
-                    row(i);
-                    row(i + 1);
+            auto rows = [&](auto hops_c) {
+                if constexpr (TWO_ROWS) {
+                    for (; i + 1 < L; i += 2) {
+                        row(i, hops_c);
+                        row(i + 1, hops_c);
+                    }
                 }
+                for (; i < L; ++i) row(i, hops_c);
+            };
+            // the row loop compiled twice where the hops apply, chosen per sequence (a scalar branch outside
+            // the loop: a per-row branch between the two lazy-F forms cost ~3% on both)
+            if constexpr (kEarlyHops > 1) {
+                if (few) rows(std::true_type{});
+                else rows(std::false_type{});
+            } else {
+                rows(std::false_type{});
             }
-            for (; i < L; ++i) row(i);
             const float sc = (sameEJ ? J : msvk::group_max<64>(Cp)) + move;
             if (lane == 0) {
                 if (maxcode >= 20u) {
