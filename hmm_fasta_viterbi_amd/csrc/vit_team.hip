@@ -102,7 +102,7 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     constexpr int VL = W * kLanes;   // virtual lanes of a team
     constexpr int ROW2 = C2 * VL;    // float2 per table row
 #ifdef VIT_TEAM_TWO_ROWS
-    constexpr bool TWO_ROWS = true;
+    constexpr bool TWO_ROWS = W > 1;  // (A/B: W = 1 S = 22 spills 20 VGPRs with two rows per trip)
 #else
     constexpr bool TWO_ROWS = false;
 #endif
