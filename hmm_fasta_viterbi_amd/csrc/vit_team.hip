@@ -101,10 +101,13 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     constexpr int C2 = (S + 1) / 2;  // float2 chunks per lane (an odd S leaves the last .y unused)
     constexpr int VL = W * kLanes;   // virtual lanes of a team
     constexpr int ROW2 = C2 * VL;    // float2 per table row
-#ifdef VIT_TEAM_TWO_ROWS
-    constexpr bool TWO_ROWS = W > 1;  // (A/B: W = 1 S = 22 spills 20 VGPRs with two rows per trip)
+    // Rows two per loop trip (the one-row loop copies values at its back edge) for the teams with phase-A
+    // transitions in LDS: cfg5's survivors -2.9% (profiles/r05_ab_vit_team_two_rows.jsonl); the W = 1 S = 22
+    // pick and the all-VGPR teams spill with two rows' register assignments (20-29 VGPRs).
+#ifdef VIT_TEAM_ONE_ROW
+    constexpr bool TWO_ROWS = false;  // (A/B base)
 #else
-    constexpr bool TWO_ROWS = false;
+    constexpr bool TWO_ROWS = W > 1 && LA > 0;
 #endif
     __shared__ float2 etab_s[ELDS ? kRows * ROW2 : 1];
     // phase A's pairs as float4 {MM, IM} and {MI, II} per chunk (one ds_read_b128 each), DM_IN as float2
