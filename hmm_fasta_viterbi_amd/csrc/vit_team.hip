@@ -106,6 +106,8 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     // pick and the all-VGPR teams spill with two rows' register assignments (20-29 VGPRs).
 #ifdef VIT_TEAM_ONE_ROW
     constexpr bool TWO_ROWS = false;  // (A/B base)
+#elif defined(VIT_TEAM_TWO_ROWS_W1)
+    constexpr bool TWO_ROWS = LA > 0;  // (A/B: the W = 1 picks too)
 #else
     constexpr bool TWO_ROWS = W > 1 && LA > 0;
 #endif
