@@ -582,7 +582,7 @@ const VitVariant* vit_team_variants(int* count) {
         VIT_TEAM(2, 11, true, 6, false, "vit_w2_s11_e"),
         VIT_TEAM(2, 11, false, 6, false, "vit_w2_s11_g"),
         VIT_TEAM(2, 12, true, 6, false, "vit_w2_s12_e"),
-        VIT_TEAM(2, 12, false, 6, true, "vit_w2_s12_g"),
+        VIT_TEAM(2, 12, false, 6, false, "vit_w2_s12_g"),
         VIT_TEAM(4, 10, false, 3, false, "vit_w4_s10_g"),
         // two waves per SIMD (<= 256 VGPRs): 8-wave workgroups of 4 teams; match scores in LDS while the
         // table fits (S <= 14), else from L2
@@ -604,14 +604,19 @@ const VitVariant* vit_team_variants(int* count) {
         // S = 19 -- the picks from S = 15 (profiles/r05_team_tune_bands_la.jsonl: 1901.hmm 2.55 vs 2.85 ms,
         // 2138 / 2207.hmm -3.5 / -5%, cfg5's survivors 21.5 vs 22.6 ms)
         VIT_TEAM_LA(2, 12, false, 6, 1, false, "vit_w2_s12_ga"),
-        VIT_TEAM_LA(2, 13, false, 6, 1, true, "vit_w2_s13_ga"),
+        VIT_TEAM_LA(2, 13, false, 6, 1, false, "vit_w2_s13_ga"),
         VIT_TEAM_LA(2, 14, false, 6, 1, true, "vit_w2_s14_ga"),
         VIT_TEAM_LA(2, 16, false, 6, 2, false, "vit_w2_s16_gb"),
         // ... and four waves per SIMD (<= 128 VGPRs, 16-wave workgroups of 8 teams) for the smaller rows
         VIT_TEAM_LA(2, 11, true, 8, 1, false, "vit_w2_s11_ea4"),
         VIT_TEAM_LA(2, 11, false, 8, 1, false, "vit_w2_s11_ga4"),
         VIT_TEAM_LA(2, 11, true, 6, 1, false, "vit_w2_s11_ea"),
-        VIT_TEAM_LA(2, 12, false, 8, 1, false, "vit_w2_s12_ga4"),
+        // the S = 12 and 13 picks since the LA teams run two rows per trip (four waves per SIMD, a few spilled
+        // VGPRs): 1509.hmm 1.90-1.94 vs 2.22-2.30 ms (w2_s12_g), 1600.hmm 2.11 vs 2.19 ms (w2_s13_ga); at S = 14
+        // the spills win (3.29 vs 2.40 ms) -- profiles/r05_team_tune_s12_two_rows.jsonl
+        VIT_TEAM_LA(2, 12, false, 8, 1, true, "vit_w2_s12_ga4"),
+        VIT_TEAM_LA(2, 13, false, 8, 1, true, "vit_w2_s13_ga4"),
+        VIT_TEAM_LA(2, 14, false, 8, 1, false, "vit_w2_s14_ga4"),
         // W = 1 (one wave per sequence, no exchange): the team kernel's row (phase A / B) with the phase-A
         // transitions (and DM_IN) in LDS, for three waves per SIMD where vit_kernel.hip fits two
         VIT_TEAM_LA(1, 22, true, 12, 2, false, "vit_w1_s22_eb"),
