@@ -110,6 +110,7 @@ class VitInfo(C.Structure):
         ("device", C.c_int),
         ("waves_per_sequence", C.c_uint32),
         ("variant", C.c_char * 64),
+        ("scratch_bytes", C.c_uint32),
     ]
 
     def as_dict(self) -> dict:

@@ -391,6 +391,8 @@ msv_status msv_vit_profile_describe(const msv_vit_profile* p, msv_vit_info* out)
     out->max_length = p->lentab_n ? p->lentab_n - 1 : 0;
     out->device = p->device;
     std::snprintf(out->variant, sizeof(out->variant), "%s", p->v->name);
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, p->v->fn) == hipSuccess) out->scratch_bytes = static_cast<uint32_t>(fa.localSizeBytes);
     return MSV_OK;
 }
 

@@ -185,7 +185,9 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
             // than the old ones (the old M(k) is read after the new one is made), so a one-row loop copied
             // the whole row back at its back edge (22 v_mov per row at S = 22); over two rows the values
             // return to their registers by themselves.
-            auto row = [&](uint64_t i, auto hops_c) {  // hops_c: std::bool_constant, the short-row hops
+            // (always_inline: the row must be inlined into both loops for its arrays to stay in registers -- left to
+            // the inliner, the second copy of the loop put M / I / D of S >= 14 in scratch, 40x slower)
+            auto row = [&](uint64_t i, auto hops_c) __attribute__((always_inline)) {  // hops_c: the short-row hops
                 const uint32_t ph = static_cast<uint32_t>(i) & 63u;
                 if (ph == 0 && i != 0) {
                     cur = nxt;
@@ -408,7 +410,7 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
                 B = fmaxf(N, J) + move;
             };
             uint64_t i = 0;
-            auto rows = [&](auto hops_c) {
+            auto rows = [&](auto hops_c) __attribute__((always_inline)) {
                 if constexpr (TWO_ROWS) {
                     for (; i + 1 < L; i += 2) {
                         row(i, hops_c);

@@ -374,6 +374,8 @@ typedef struct msv_vit_info {
     int device;
     uint32_t waves_per_sequence; /* 1, or a team of waves sharing one sequence's row (vit_team.hip) */
     char variant[64];
+    uint32_t scratch_bytes;   /* private (scratch) memory per lane of the variant's kernel: spills or
+                                 arrays the compiler could not keep in registers (0 for a healthy variant) */
 } msv_vit_info;
 msv_status msv_vit_profile_describe(const msv_vit_profile* profile, msv_vit_info* out);
 int msv_vit_variant_count(void);

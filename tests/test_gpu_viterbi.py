@@ -475,3 +475,27 @@ def test_timeline_stamps_leave_scores_unchanged(name):
     assert np.array_equal(seq[:, 3].astype(np.int64), lens[live])
     used = x[n:][x[n:, 2] > 0]
     assert len(used) >= 1 and np.all(used[:, 0] <= used[:, 1]) and np.all(used[:, 1] <= used[:, 2])
+
+
+def test_no_variant_keeps_its_rows_in_scratch():
+    """Every compiled Viterbi variant keeps its DP rows in registers: its kernel's private (scratch) memory per
+    lane is at most a few spilled values.  A variant whose M / I / D arrays went to scratch still scores
+    bitwise and is ~40x slower (round 5: a second instantiation of the single-wave row loop did that to
+    S = 14..24 until the row lambdas were forced inline).  Pre-existing spills of the non-pick variants that
+    run past the register file (S >= 32 at two waves per SIMD) stay below 1.2 KB and are listed here."""
+    # (round 5 build: bytes of private memory per lane, i.e. spilled VGPRs x 4 -- x 1.5 headroom)
+    allowed = {name: int(b * 1.5) for name, b in {
+        "vit_s24_t5": 36, "vit_s32_t0gi": 108, "vit_s38_t0g": 132, "vit_s38_t0ga": 260, "vit_s38_t0gi": 288,
+        "vit_s48_t0g": 408, "vit_s48_t7gw4": 184, "vit_s64_t0g": 880, "vit_s64_t0gi": 1132,
+        "vit_w2_s12_ga4": 20, "vit_w2_s13_ga4": 40, "vit_w2_s14_ga4": 76, "vit_w1_s22_ea": 36, "vit_w1_s22_gb": 36,
+        "vit_w1_s22_e": 40, "vit_w1_s16_ea4": 44}.items()}
+    prof = "100.hmm"
+    bad = {}
+    for name in msv.Viterbi_HMM.variants():
+        e = msv.Viterbi_HMM(hmm(prof), insert_mode=1 if name.endswith("i") else 0)
+        e.set_variant(name)
+        info = e.describe()
+        assert info["variant"] == name
+        if info["scratch_bytes"] > allowed.get(name, 0):
+            bad[name] = info["scratch_bytes"]
+    assert not bad, bad
