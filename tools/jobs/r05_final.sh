@@ -3,7 +3,7 @@
 # picks on their survivors (cfg3 vit_w1_s22_ea, cfg5 vit_w2_s19_gb).
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r05_final2
+O=gpurun_out/r05_final3
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
 timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
