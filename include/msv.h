@@ -372,10 +372,11 @@ typedef struct msv_vit_info {
     uint32_t lds_bytes;
     uint32_t max_length;
     int device;
-    uint32_t waves_per_sequence; /* 1, or a team of waves sharing one sequence's row (vit_team.hip) */
     char variant[64];
+    /* appended fields (append-only: the round-4 prefix above keeps its offsets) */
     uint32_t scratch_bytes;   /* private (scratch) memory per lane of the variant's kernel: spills or
                                  arrays the compiler could not keep in registers (0 for a healthy variant) */
+    uint32_t waves_per_sequence; /* 1, or a team of waves sharing one sequence's row (vit_team.hip) */
 } msv_vit_info;
 msv_status msv_vit_profile_describe(const msv_vit_profile* profile, msv_vit_info* out);
 int msv_vit_variant_count(void);

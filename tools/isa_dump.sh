@@ -1,5 +1,5 @@
 #!/bin/bash
-# Dump the gfx950 assembly of every MSV kernel translation unit into $1 (one .s per TU), for
+# Dump the gfx950 assembly of every MSV and Viterbi kernel translation unit into $1 (one .s per TU), for
 # instruction-for-instruction comparisons of a source change (tools/isa_compare.py).
 set -e
 OUT=${1:?usage: tools/isa_dump.sh OUTDIR}
@@ -12,4 +12,6 @@ for k in 0 1 2 3 4 5 6 7; do
 done
 /opt/rocm/bin/hipcc $FLAGS "$HERE/msv_kernel.hip" -o "$OUT/msv_kernel.s" &
 /opt/rocm/bin/hipcc $FLAGS "$HERE/msv_coop.hip" -o "$OUT/msv_coop.s" &
+/opt/rocm/bin/hipcc $FLAGS "$HERE/vit_kernel.hip" -o "$OUT/vit_kernel.s" &
+/opt/rocm/bin/hipcc $FLAGS "$HERE/vit_team.hip" -o "$OUT/vit_team.s" &
 wait
