@@ -108,9 +108,9 @@ class VitInfo(C.Structure):
         ("lds_bytes", C.c_uint32),
         ("max_length", C.c_uint32),
         ("device", C.c_int),
-        ("waves_per_sequence", C.c_uint32),
         ("variant", C.c_char * 64),
         ("scratch_bytes", C.c_uint32),
+        ("waves_per_sequence", C.c_uint32),
     ]
 
     def as_dict(self) -> dict:

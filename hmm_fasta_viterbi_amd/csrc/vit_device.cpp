@@ -392,7 +392,10 @@ msv_status msv_vit_profile_describe(const msv_vit_profile* p, msv_vit_info* out)
     out->device = p->device;
     std::snprintf(out->variant, sizeof(out->variant), "%s", p->v->name);
     hipFuncAttributes fa{};
-    if (hipFuncGetAttributes(&fa, p->v->fn) == hipSuccess) out->scratch_bytes = static_cast<uint32_t>(fa.localSizeBytes);
+    if (hipFuncGetAttributes(&fa, p->v->fn) == hipSuccess) {
+        out->scratch_bytes = static_cast<uint32_t>(fa.localSizeBytes);
+        out->lds_bytes = static_cast<uint32_t>(fa.sharedSizeBytes);  // the kernel's own static LDS, exactly
+    }
     return MSV_OK;
 }
 

@@ -46,11 +46,8 @@ namespace {
 
 constexpr float NINF = -__builtin_inff();
 constexpr int kEarlyD = 8;  // slots of the unconditional first lazy-F pass before its early-exit test
-#ifndef VIT_EARLY_HOP_STATES
-#define VIT_EARLY_HOP_STATES 8
-#endif
 // rows of S < kEarlyD: states (over whole-lane hops) of the unconditional first lazy-F passes
-constexpr int kEarlyHopStates = VIT_EARLY_HOP_STATES;
+constexpr int kEarlyHopStates = 8;
 
 __device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 __device__ __forceinline__ uint64_t u64first(uint64_t x) {
@@ -104,7 +101,14 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
     const int lane = threadIdx.x & 63;
     // (readfirstlane: wave-uniform, so the sequence, its bounds and every branch on them are scalar)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t total = a.select_count ? static_cast<uint64_t>(*a.select_count) : a.n;
+    // the list's length, at most n: a device count beyond the batch is latched (kErrBadOrder) and clamped, so no
+    // wave reads the list past its n entries
+    uint64_t total = a.n;
+    if (a.select_count) {
+        const uint64_t c = *a.select_count;
+        if (c > a.n && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.errors, msvk::kErrBadOrder);
+        total = c < a.n ? c : a.n;
+    }
     if (static_cast<uint64_t>(blockIdx.x) * WAVES >= total) {
         // no sequence for this workgroup (a device-count launch is sized for n, the count may be far less:
         // cfg2's 260 survivors of 10,000): no first item, and none of the queue's (it starts at the grid's
@@ -457,9 +461,10 @@ __global__ __launch_bounds__(WAVES * 64) void vit_kernel(const VitArgs a) {
 
 // ------------------------------------------------------------------------------------------------
 // MSV filter survivors: the P-value of every score and a STABLE stream compaction of the sequences with
-// P <= threshold, in the given dequeue order -- two launches of 256 entries per block: (1) P-values and each
-// block's survivor count, (2) each block sums the counts before it and writes its survivors at their exact
-// rank.  With the MSV launch's longest-first order the Viterbi launch then takes its survivors exactly
+// P <= threshold, in the given dequeue order -- three launches: (1) P-values and each 256-entry block's
+// survivor count, (2) one workgroup turns the counts into exclusive prefixes (and the total), (3) each block
+// writes its survivors at their exact rank.  O(n) in all (round 5 summed every block's predecessors in (3),
+// O(blocks^2)).  With the MSV launch's longest-first order the Viterbi launch then takes its survivors exactly
 // longest first, so its drain tail is its shortest sequences (an unordered append -- one atomic per wave,
 // stretches of 64 in arrival order -- left long survivors in the last round of the persistent grid:
 // cfg3 1.40 vs 1.26 ms, cfg5 21.6 vs 20.0 ms with the team kernels, profiles/r05_select_order.jsonl).
@@ -505,19 +510,41 @@ __global__ __launch_bounds__(kSelBlock) void vit_select_count_kernel(const float
     if (threadIdx.x == 0) block_counts[blockIdx.x] = c;
 }
 
+// Exclusive prefix sums of the block counts in place, and the total into *count: one workgroup, each thread a
+// contiguous run of the counts (blocks <= 2^24 for n < 2^32, so a run is <= 16,384 entries).
+constexpr int kScanBlock = 1024;
+__global__ __launch_bounds__(kScanBlock) void vit_select_scan_kernel(uint32_t* __restrict__ block_counts,
+                                                                    uint32_t blocks, uint32_t* __restrict__ count) {
+    __shared__ uint32_t part_s[kScanBlock];
+    const uint32_t per = (blocks + kScanBlock - 1) / kScanBlock;
+    const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < blocks ? b0 + per : blocks;
+    uint32_t sum = 0;
+    for (uint32_t j = b0; j < b1; ++j) sum += block_counts[j];
+    part_s[threadIdx.x] = sum;
+    __syncthreads();
+    // Hillis-Steele inclusive scan of the 1,024 run sums
+    for (int d = 1; d < kScanBlock; d <<= 1) {
+        const uint32_t v = threadIdx.x >= static_cast<uint32_t>(d) ? part_s[threadIdx.x - d] : 0u;
+        __syncthreads();
+        part_s[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part_s[threadIdx.x] - sum;  // exclusive
+    for (uint32_t j = b0; j < b1; ++j) {
+        const uint32_t c = block_counts[j];
+        block_counts[j] = run;
+        run += c;
+    }
+    if (threadIdx.x == kScanBlock - 1) *count = part_s[kScanBlock - 1];
+}
+
 __global__ __launch_bounds__(kSelBlock) void vit_select_write_kernel(const float* __restrict__ scores,
                                                                      const uint64_t* __restrict__ offsets,
                                                                      const uint32_t* __restrict__ order, uint64_t n,
                                                                      float mu, float lambda, double threshold,
-                                                                     const uint32_t* __restrict__ block_counts,
-                                                                     uint32_t* __restrict__ select,
-                                                                     uint32_t* __restrict__ count) {
-    __shared__ uint32_t lds4[4];
+                                                                     const uint32_t* __restrict__ block_prefix,
+                                                                     uint32_t* __restrict__ select) {
     __shared__ uint32_t wave_base[4];
-    // survivors of the blocks before this one
-    uint32_t part = 0;
-    for (uint32_t j = threadIdx.x; j < blockIdx.x; j += kSelBlock) part += block_counts[j];
-    const uint32_t prefix = block_sum(part, lds4);
     uint32_t idx = 0;
     const uint64_t pos = static_cast<uint64_t>(blockIdx.x) * kSelBlock + threadIdx.x;
     const bool pass = select_pass(scores, offsets, order, n, mu, lambda, threshold, nullptr, pos, &idx);
@@ -527,11 +554,9 @@ __global__ __launch_bounds__(kSelBlock) void vit_select_write_kernel(const float
                                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(mask), 0u));
     if (lane == 0) wave_base[wv] = static_cast<uint32_t>(__popcll(mask));
     __syncthreads();
-    uint32_t base = prefix;
+    uint32_t base = block_prefix[blockIdx.x];
     for (uint32_t k = 0; k < wv; ++k) base += wave_base[k];
     if (pass) select[base + below] = idx;
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
-        *count = prefix + wave_base[0] + wave_base[1] + wave_base[2] + wave_base[3];
 }
 
 hipError_t launch_select(const float* scores, const uint64_t* offsets, const uint32_t* order, uint64_t n, float mu,
@@ -540,19 +565,37 @@ hipError_t launch_select(const float* scores, const uint64_t* offsets, const uin
     const uint64_t blocks = (n + kSelBlock - 1) / kSelBlock;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     if (blocks == 0) return hipMemsetAsync(count, 0, sizeof(uint32_t), stream);
-    // the per-block counts: stream-ordered scratch, so calls on different streams never share it
+    // the per-block counts: stream-ordered scratch, so calls on different streams never share it; a device
+    // without memory pools gets a plain allocation, freed after the stream has drained
+    int dev = 0, pools = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&pools, hipDeviceAttributeMemoryPoolsSupported, dev);
+    if (e != hipSuccess) return e;
     uint32_t* counts = nullptr;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&counts), blocks * sizeof(uint32_t), stream);
+    e = pools ? hipMallocAsync(reinterpret_cast<void**>(&counts), blocks * sizeof(uint32_t), stream)
+              : hipMalloc(reinterpret_cast<void**>(&counts), blocks * sizeof(uint32_t));
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(vit_select_count_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kSelBlock), 0, stream,
                        scores, offsets, order, n, mu, lambda, threshold, pvalues, counts);
     e = hipGetLastError();
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(vit_select_write_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kSelBlock), 0, stream,
-                           scores, offsets, order, n, mu, lambda, threshold, counts, select, count);
+        hipLaunchKernelGGL(vit_select_scan_kernel, dim3(1), dim3(kScanBlock), 0, stream, counts,
+                           static_cast<uint32_t>(blocks), count);
         e = hipGetLastError();
     }
-    const hipError_t f = hipFreeAsync(counts, stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(vit_select_write_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kSelBlock), 0, stream,
+                           scores, offsets, order, n, mu, lambda, threshold, counts, select);
+        e = hipGetLastError();
+    }
+    hipError_t f;
+    if (pools) {
+        f = hipFreeAsync(counts, stream);
+    } else {
+        f = hipStreamSynchronize(stream);
+        const hipError_t g = hipFree(counts);
+        f = f != hipSuccess ? f : g;
+    }
     return e != hipSuccess ? e : f;
 }
 
@@ -574,11 +617,12 @@ hipError_t launch_select(const float* scores, const uint64_t* offsets, const uin
                (ELDS_ ? kRows * (S_)*kLanes * 4 : 0) + (kTransitions - (NT_)) * (S_)*kLanes * 4}
 
 // `P` marks the automatic choice per S (interleaved timings on the MSV survivors of cfg3 / cfg5 and on cfg2,
-// profiles/r04_vit_tune_cfg{2,3,5}.jsonl); `-` are the A/B candidates kept selectable by name.  Round 5: the
-// team variants (vit_team.hip) took over 1,409-1,920 and 2,049-2,432 states
-// (profiles/r05_team_tune_bands.jsonl: 1509.hmm 2.02 vs 2.23 ms, 1901.hmm 2.78 vs 2.82, 2050-2365.hmm
-// 27-32% faster; cfg5's survivors 22.2 vs 33.7 ms; 1600 / 1705.hmm -4 / -6%, profiles/r05_team_tune_bands_s13s14.jsonl),
-// so s24..s30_t0g and s34/36/38_t7gw4 are no longer picks.
+// profiles/r04_vit_tune_cfg{2,3,5}.jsonl); round 5's team variants (vit_team.hip) took over 1,281-1,920 and
+// 2,049-2,432 states (profiles/r05_team_tune_bands*.jsonl).  Round 6 pruned the table to the picks, which
+// also serve as the fallback of every wider band (set_variant accepts any variant whose S covers the model),
+// plus vit_s22_t5a, the single-wave form of the 1,281-1,408 band (the team pick's A/B base).  The ~30 A/B-only
+// forms (t5 / t0 splits, descending rows, one wave per SIMD with every transition in VGPRs) are in git history
+// up to round 5, with their timings in profiles/r04_vit_tune_*.jsonl.
 #define P true
 #define X false
 static const VitVariant* single_wave_variants(int* count) {
@@ -593,48 +637,14 @@ static const VitVariant* single_wave_variants(int* count) {
         VIT_VARIANT(14, 7, true, false, 8, 0, false, P, "vit_s14_t7"),
         VIT_VARIANT(16, 7, true, false, 8, 0, false, P, "vit_s16_t7"),
         VIT_VARIANT(18, 7, true, false, 8, 0, false, P, "vit_s18_t7"),
-        // five arrays in VGPRs, the D chain's two (MD, DD) in LDS
-        VIT_VARIANT(16, 5, true, false, 8, 1, false, X, "vit_s16_t5"),
-        VIT_VARIANT(18, 5, true, false, 8, 1, false, X, "vit_s18_t5"),
-        VIT_VARIANT(20, 5, true, false, 8, 1, false, X, "vit_s20_t5"),
-        VIT_VARIANT(22, 5, true, false, 8, 1, false, X, "vit_s22_t5"),
-        VIT_VARIANT(24, 5, true, false, 8, 1, false, X, "vit_s24_t5"),
-        // every transition array in LDS, match scores in LDS
-        VIT_VARIANT(16, 0, true, false, 8, 1, false, X, "vit_s16_t0"),
-        VIT_VARIANT(22, 0, true, false, 8, 1, false, X, "vit_s22_t0"),
-        // transitions in LDS, match scores from L2
-        VIT_VARIANT(24, 0, false, false, 8, 3, false, X, "vit_s24_t0g"),
-        VIT_VARIANT(26, 0, false, false, 8, 3, false, X, "vit_s26_t0g"),
-        VIT_VARIANT(28, 0, false, false, 8, 3, false, X, "vit_s28_t0g"),
-        VIT_VARIANT(30, 0, false, false, 8, 3, false, X, "vit_s30_t0g"),
-        VIT_VARIANT(32, 0, false, false, 8, 3, false, P, "vit_s32_t0g"),
-        VIT_VARIANT(38, 0, false, false, 8, 3, false, X, "vit_s38_t0g"),
-        VIT_VARIANT(48, 0, false, false, 8, 3, false, X, "vit_s48_t0g"),
-        VIT_VARIANT(64, 0, false, false, 8, 3, false, P, "vit_s64_t0g"),
-        // the row as one ascending pass (D chain interleaved with the M/I work): cfg3 1.68 vs 1.85 ms at S = 22
-        VIT_VARIANT(8, 7, true, false, 8, 0, true, X, "vit_s8_t7a"),
-        VIT_VARIANT(16, 7, true, false, 8, 0, true, X, "vit_s16_t7a"),
-        VIT_VARIANT(18, 7, true, false, 8, 0, true, X, "vit_s18_t7a"),
+        // five arrays in VGPRs (MD, DD in LDS), the row as one ascending pass: cfg3 1.68 vs 1.85 ms at S = 22
         VIT_VARIANT(20, 5, true, false, 8, 1, true, P, "vit_s20_t5a"),
         VIT_VARIANT(22, 5, true, false, 8, 1, true, X, "vit_s22_t5a"),
-        VIT_VARIANT(22, 0, true, false, 8, 1, true, X, "vit_s22_t0a"),
-        VIT_VARIANT(38, 0, false, false, 8, 3, true, X, "vit_s38_t0ga"),
-        // one wave per SIMD (4 per workgroup): the 512-register budget holds S = 38 without the 52 spilled
-        // VGPRs of the 8-wave form (S = 48: 12 instead of 169)
-        VIT_VARIANT(38, 0, false, false, 4, 1, false, X, "vit_s38_t0g4"),
+        // transitions in LDS, match scores from L2 (two waves per SIMD; S = 64 spills, models > 3,072 states only)
+        VIT_VARIANT(32, 0, false, false, 8, 3, false, P, "vit_s32_t0g"),
+        VIT_VARIANT(64, 0, false, false, 8, 3, false, P, "vit_s64_t0g"),
+        // one wave per SIMD (4 per workgroup): the 512-register budget holds S = 48 with 12 spilled VGPRs
         VIT_VARIANT(48, 0, false, false, 4, 3, false, P, "vit_s48_t0g4"),
-        // one wave per SIMD with every transition array in registers (no transition reads from LDS): slower
-        // than two waves per SIMD where those fit without spilling (S = 22-32), faster where they spill (34-38)
-        VIT_VARIANT(16, 7, true, false, 4, 0, false, X, "vit_s16_t7w4"),
-        VIT_VARIANT(22, 7, true, false, 4, 0, false, X, "vit_s22_t7w4"),
-        VIT_VARIANT(22, 7, true, false, 4, 0, true, X, "vit_s22_t7w4a"),
-        VIT_VARIANT(24, 7, true, false, 4, 0, false, X, "vit_s24_t7w4"),
-        VIT_VARIANT(26, 7, true, false, 4, 0, false, X, "vit_s26_t7w4"),
-        VIT_VARIANT(28, 7, true, false, 4, 0, false, X, "vit_s28_t7w4"),
-        VIT_VARIANT(34, 7, false, false, 4, 3, false, X, "vit_s34_t7gw4"),
-        VIT_VARIANT(36, 7, false, false, 4, 3, false, X, "vit_s36_t7gw4"),
-        VIT_VARIANT(38, 7, false, false, 4, 3, false, X, "vit_s38_t7gw4"),
-        VIT_VARIANT(48, 7, false, false, 4, 3, false, X, "vit_s48_t7gw4"),
         // informative insert scores (insert_mode 1): transitions in LDS, match and insert scores from L2
         VIT_VARIANT(2, 0, false, true, 8, 3, false, P, "vit_s2_t0gi"),
         VIT_VARIANT(8, 0, false, true, 8, 3, false, P, "vit_s8_t0gi"),
@@ -642,8 +652,7 @@ static const VitVariant* single_wave_variants(int* count) {
         VIT_VARIANT(22, 0, false, true, 8, 3, false, P, "vit_s22_t0gi"),
         VIT_VARIANT(28, 0, false, true, 8, 3, false, P, "vit_s28_t0gi"),
         VIT_VARIANT(32, 0, false, true, 8, 3, false, P, "vit_s32_t0gi"),
-        VIT_VARIANT(38, 0, false, true, 8, 3, false, X, "vit_s38_t0gi"),
-        // ... one wave per SIMD where two spill (the zero-insert picks' form)
+        // ... one wave per SIMD with every transition in VGPRs where two waves spill
         VIT_VARIANT(34, 7, false, true, 4, 3, false, P, "vit_s34_t7gw4i"),
         VIT_VARIANT(38, 7, false, true, 4, 3, false, P, "vit_s38_t7gw4i"),
         VIT_VARIANT(64, 0, false, true, 8, 3, false, P, "vit_s64_t0gi"),

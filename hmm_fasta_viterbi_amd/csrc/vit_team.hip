@@ -49,10 +49,7 @@ namespace vitk {
 namespace {
 
 constexpr float TNINF = -__builtin_inff();
-#ifndef VIT_TEAM_EARLY_D
-#define VIT_TEAM_EARLY_D 8
-#endif
-constexpr int kTeamEarlyD = VIT_TEAM_EARLY_D;  // slots of the unconditional first lazy-F pass (vit_kernel.hip kEarlyD)
+constexpr int kTeamEarlyD = 8;  // slots of the unconditional first lazy-F pass (vit_kernel.hip kEarlyD)
 constexpr int DPP_WSHR1 = 0x138;
 // A poll that spins this long means the team's protocol broke (a bug, never data): the wave latches
 // kErrTeamHang and leaves the kernel instead of holding the GPU (each poll is one LDS round trip, so this is
@@ -104,13 +101,7 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     // Rows two per loop trip (the one-row loop copies values at its back edge) for the teams with phase-A
     // transitions in LDS: cfg5's survivors -2.9% (profiles/r05_ab_vit_team_two_rows.jsonl); the W = 1 S = 22
     // pick and the all-VGPR teams spill with two rows' register assignments (20-29 VGPRs).
-#ifdef VIT_TEAM_ONE_ROW
-    constexpr bool TWO_ROWS = false;  // (A/B base)
-#elif defined(VIT_TEAM_TWO_ROWS_W1)
-    constexpr bool TWO_ROWS = LA > 0;  // (A/B: the W = 1 picks too)
-#else
     constexpr bool TWO_ROWS = W > 1 && LA > 0;
-#endif
     __shared__ float2 etab_s[ELDS ? kRows * ROW2 : 1];
     // phase A's pairs as float4 {MM, IM} and {MI, II} per chunk (one ds_read_b128 each), DM_IN as float2
     __shared__ float4 tpa_s[LA ? 2 * C2 * VL : 1];
@@ -118,7 +109,14 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
     __shared__ float4 tdm_s[LA == 2 ? C4 * VL : 1];
     __shared__ TeamX<W> tx_s[NT];
     const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();  // (a.stamps only)
-    const uint64_t total = a.select_count ? static_cast<uint64_t>(*a.select_count) : a.n;
+    // the list's length, at most n: a device count beyond the batch is latched (kErrBadOrder) and clamped, so no
+    // wave reads the list past its n entries
+    uint64_t total = a.n;
+    if (a.select_count) {
+        const uint64_t c = *a.select_count;
+        if (c > a.n && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.errors, msvk::kErrBadOrder);
+        total = c < a.n ? c : a.n;
+    }
     if (static_cast<uint64_t>(blockIdx.x) * NT >= total) {
         // no sequence for this workgroup (vit_kernel.hip: a device-count launch sized for n): leave at once,
         // counted as its NT * W waves
@@ -385,22 +383,10 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                     }
                     // J(i-1) from every wave's E record (the ballot used the same J + loop), N, B
                     const float Jn = J + loop;
-#ifdef VIT_AB_NO_CHAIN
-                    // timing-only A/B build (scores differ on rows where J rises): B from the J of one row
-                    // earlier, so the row's B no longer waits for its E (the B -> cells -> E -> J -> B chain gets
-                    // a row of slack) while J, and so the E ballot's rare path, stay as they are -- bounds what
-                    // taking E off the chain can gain
-                    const float Jold = J;
-                    J = fmaxf(Jn, wait_e(Ew, st) + tEJ);
-                    if (hung) return false;
-                    N = N + loop;
-                    B = fmaxf(N, Jold + loop) + move;
-#else
                     J = fmaxf(Jn, wait_e(Ew, st) + tEJ);
                     if (hung) return false;
                     N = N + loop;
                     B = fmaxf(N, J) + move;
-#endif
                 }
                 const float Bt = B + tBM;
                 // ---- phase B: row i.  Slot 0 reads the previous row's state k0-1 through the lane shift (lane
@@ -571,69 +557,33 @@ __global__ __launch_bounds__(NT * W * 64) void vit_team_kernel(const VitArgs a) 
                reinterpret_cast<const void*>(&vit_team_kernel<W_, S_, ELDS_, NT_, LA_>),               \
                NAME_,                                                                                  \
                (ELDS_ ? kRows * ((S_) + 1) / 2 * (W_) * kLanes * 8 : 0) +                              \
-                   ((LA_) == 2 ? 5 : (LA_) == 1 ? 4 : 0) * (((S_) + 1) / 2) * (W_) * kLanes * 8 +          \
+                   ((LA_) ? 4 * (((S_) + 1) / 2) * (W_) * kLanes * 8 : 0) +                              \
+                   ((LA_) == 2 ? (((S_) + 1) / 2 + 1) / 2 * (W_) * kLanes * 16 : 0) +                         \
                    (NT_) * static_cast<int>(sizeof(TeamX<W_>)),                                        \
                W_}
 #define VIT_TEAM(W_, S_, ELDS_, NT_, PICK_, NAME_) VIT_TEAM_LA(W_, S_, ELDS_, NT_, 0, PICK_, NAME_)
 
+// Round 6 keeps the band picks (`true`) and two W = 2 forms with every transition in VGPRs (the timeline test's
+// and tools/vit_concurrent.py's tail companion); the other ~35 round-5 A/B forms (W = 3 / 4, match scores in
+// LDS, one-row loops, the W = 1 S = 12..20 rows) are in git history with their timings in
+// profiles/r05_team_tune_*.jsonl.
 const VitVariant* vit_team_variants(int* count) {
     static const VitVariant all[] = {
-        // three waves per SIMD (<= 168 VGPRs): 12-wave workgroups of 6 teams
-        VIT_TEAM(2, 11, true, 6, false, "vit_w2_s11_e"),
+        // three waves per SIMD (<= 168 VGPRs): a 12-wave workgroup of 6 teams, and a one-team workgroup
         VIT_TEAM(2, 11, false, 6, false, "vit_w2_s11_g"),
-        VIT_TEAM(2, 12, true, 6, false, "vit_w2_s12_e"),
-        VIT_TEAM(2, 12, false, 6, false, "vit_w2_s12_g"),
-        VIT_TEAM(4, 10, false, 3, false, "vit_w4_s10_g"),
-        // two waves per SIMD (<= 256 VGPRs): 8-wave workgroups of 4 teams; match scores in LDS while the
-        // table fits (S <= 14), else from L2
-        VIT_TEAM(2, 13, true, 4, false, "vit_w2_s13_e"),
-        VIT_TEAM(2, 14, true, 4, false, "vit_w2_s14_e"),
-        VIT_TEAM(2, 13, false, 4, false, "vit_w2_s13_g"),
-        VIT_TEAM(2, 14, false, 4, false, "vit_w2_s14_g"),
-        VIT_TEAM(2, 15, false, 4, false, "vit_w2_s15_g"),
-        VIT_TEAM(2, 16, false, 4, false, "vit_w2_s16_g"),
-        VIT_TEAM(2, 17, false, 4, false, "vit_w2_s17_g"),
-        VIT_TEAM(2, 18, false, 4, false, "vit_w2_s18_g"),
-        VIT_TEAM(2, 19, false, 4, false, "vit_w2_s19_g"),
-        VIT_TEAM(3, 13, false, 2, false, "vit_w3_s13_g"),
-        // one- / two-team workgroups (tail companions: small enough to start on a CU as another launch's
-        // waves leave it)
         VIT_TEAM(2, 11, false, 1, false, "vit_w2_s11_g1"),
-        VIT_TEAM(2, 11, false, 2, false, "vit_w2_s11_g2"),
-        // phase-A transitions in LDS (and DM_IN, `gb`): three waves per SIMD for the two-wave teams up to
-        // S = 19 -- the picks from S = 15 (profiles/r05_team_tune_bands_la.jsonl: 1901.hmm 2.55 vs 2.85 ms,
-        // 2138 / 2207.hmm -3.5 / -5%, cfg5's survivors 21.5 vs 22.6 ms)
-        VIT_TEAM_LA(2, 12, false, 6, 1, false, "vit_w2_s12_ga"),
-        VIT_TEAM_LA(2, 13, false, 6, 1, false, "vit_w2_s13_ga"),
-        VIT_TEAM_LA(2, 14, false, 6, 1, true, "vit_w2_s14_ga"),
-        VIT_TEAM_LA(2, 16, false, 6, 2, false, "vit_w2_s16_gb"),
-        // ... and four waves per SIMD (<= 128 VGPRs, 16-wave workgroups of 8 teams) for the smaller rows
-        VIT_TEAM_LA(2, 11, true, 8, 1, false, "vit_w2_s11_ea4"),
-        VIT_TEAM_LA(2, 11, false, 8, 1, false, "vit_w2_s11_ga4"),
-        VIT_TEAM_LA(2, 11, true, 6, 1, false, "vit_w2_s11_ea"),
-        // the S = 12 and 13 picks since the LA teams run two rows per trip (four waves per SIMD, a few spilled
-        // VGPRs): 1509.hmm 1.90-1.94 vs 2.22-2.30 ms (w2_s12_g), 1600.hmm 2.11 vs 2.19 ms (w2_s13_ga); at S = 14
-        // the spills win (3.29 vs 2.40 ms) -- profiles/r05_team_tune_s12_two_rows.jsonl
+        // W = 1 (one wave per sequence, no exchange): the team kernel's row (phase A / B) with the phase-A
+        // transitions in LDS, three waves per SIMD where vit_kernel.hip fits two -- the 1,281-1,408 pick
+        VIT_TEAM_LA(1, 22, true, 12, 1, true, "vit_w1_s22_ea"),
+        // phase-A transitions in LDS: four waves per SIMD (<= 128 VGPRs, 16-wave workgroups of 8 teams) for
+        // S = 12, 13 (1509.hmm 1.90-1.94 vs 2.22-2.30 ms, 1600.hmm 2.11 vs 2.19 ms,
+        // profiles/r05_team_tune_s12_two_rows.jsonl), three for S = 14, 15 ...
         VIT_TEAM_LA(2, 12, false, 8, 1, true, "vit_w2_s12_ga4"),
         VIT_TEAM_LA(2, 13, false, 8, 1, true, "vit_w2_s13_ga4"),
-        VIT_TEAM_LA(2, 14, false, 8, 1, false, "vit_w2_s14_ga4"),
-        // W = 1 (one wave per sequence, no exchange): the team kernel's row (phase A / B) with the phase-A
-        // transitions (and DM_IN) in LDS, for three waves per SIMD where vit_kernel.hip fits two
-        VIT_TEAM_LA(1, 22, true, 12, 2, false, "vit_w1_s22_eb"),
-        VIT_TEAM_LA(1, 22, true, 12, 1, true, "vit_w1_s22_ea"),
-        VIT_TEAM_LA(1, 22, false, 12, 2, false, "vit_w1_s22_gb"),
-        VIT_TEAM_LA(1, 20, true, 12, 2, false, "vit_w1_s20_eb"),
-        VIT_TEAM_LA(1, 22, true, 8, 0, false, "vit_w1_s22_e"),
-        VIT_TEAM_LA(1, 22, true, 8, 1, false, "vit_w1_s22_ea2"),
-        VIT_TEAM_LA(1, 20, true, 12, 1, false, "vit_w1_s20_ea"),
-        VIT_TEAM_LA(1, 18, true, 12, 1, false, "vit_w1_s18_ea"),
-        VIT_TEAM_LA(1, 16, true, 12, 1, false, "vit_w1_s16_ea"),
-        VIT_TEAM_LA(1, 14, true, 12, 1, false, "vit_w1_s14_ea"),
-        VIT_TEAM_LA(1, 12, true, 12, 1, false, "vit_w1_s12_ea"),
-        VIT_TEAM_LA(1, 16, true, 16, 1, false, "vit_w1_s16_ea4"),
-        VIT_TEAM_LA(1, 14, true, 16, 1, false, "vit_w1_s14_ea4"),
-        VIT_TEAM_LA(1, 12, true, 16, 1, false, "vit_w1_s12_ea4"),
+        VIT_TEAM_LA(2, 14, false, 6, 1, true, "vit_w2_s14_ga"),
         VIT_TEAM_LA(2, 15, false, 6, 1, true, "vit_w2_s15_ga"),
+        // ... and DM_IN in LDS too (`gb`) for S = 17..19 (profiles/r05_team_tune_bands_la.jsonl: 1901.hmm 2.55 vs
+        // 2.85 ms, 2138 / 2207.hmm -3.5 / -5%, cfg5's survivors 21.5 vs 22.6 ms)
         VIT_TEAM_LA(2, 17, false, 6, 2, true, "vit_w2_s17_gb"),
         VIT_TEAM_LA(2, 18, false, 6, 2, true, "vit_w2_s18_gb"),
         VIT_TEAM_LA(2, 19, false, 6, 2, true, "vit_w2_s19_gb"),
