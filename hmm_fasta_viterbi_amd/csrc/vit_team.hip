@@ -71,7 +71,13 @@ struct TeamX {
 };
 
 // LDS accesses of the exchange: volatile native vectors, so every poll is a fresh single ds_read and every
-// record is ONE ds_write (its stamp rides with the data: a reader that sees the stamp sees the record).
+// record is ONE ds_write (its stamp rides with the data: a reader that sees the stamp sees the record).  This
+// relies on one lane's aligned 16-byte (boundary) and 8-byte (E, next) LDS access being single-copy atomic; only
+// lane 0's copy of a boundary is used (the DPP shift's `old` for wave 1's lane 0) and lane 0's stamp is the one
+// compared.  tests/test_team_exchange_isa.py checks in the gfx950 ISA that each record is one ds_write_b128 /
+// ds_write_b64 and each poll one ds_read_b128 / ds_read_b64 comparing that load's last dword.  (Stamping every
+// 8-byte half instead, which needs only 64-bit atomicity, was built in four forms and measured 3-8% slower on
+// cfg5's survivors: profiles/r06_ab/README.md.)
 typedef float v2f __attribute__((ext_vector_type(2)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 #define LDS_AS __attribute__((address_space(3)))

@@ -376,6 +376,34 @@ def test_bad_survivor_index_is_reported():
     assert np.all(got[[i for i in range(n) if i not in (3, 7, 11)]] == 7.0)
 
 
+@pytest.mark.parametrize("prof", ["400.hmm", "1400.hmm", "2405.hmm"])  # single-wave, W = 1 team, W = 2 team picks
+def test_survivor_count_beyond_the_batch_is_clamped(prof):
+    """a device survivors count larger than n is reported (MSV_ERR_INVALID_ARGUMENT) and clamped to
+    n, so no wave reads the list past its n entries; the n listed sequences are still scored."""
+    import torch
+    e = vit(prof)
+    codes, offsets = random_batch(98, 40, 20, 300)
+    n = len(offsets) - 1
+    want = OracleProfile(prof).vit_score_batch(codes, offsets)
+    dev = torch.device("cuda:0")
+    d_res = torch.from_numpy(codes).to(dev)
+    d_off = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    # the list's n entries, then 64 more (valid indices, so only the count check can report them: a kernel that
+    # read past n would score sequence 0 again without a word)
+    sel = np.concatenate([np.arange(n, dtype=np.uint32)[::-1], np.zeros(64, np.uint32)])
+    d_sel = torch.from_numpy(sel.view(np.int32)).to(dev)
+    d_cnt = torch.tensor([n + 64], dtype=torch.int32, device=dev)
+    d_sc = torch.full((n,), 7.0, dtype=torch.float32, device=dev)
+    st = torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    e.score_batch_device(d_res.data_ptr(), codes.size, d_off.data_ptr(), n, d_sc.data_ptr(), d_sel.data_ptr(),
+                         d_cnt.data_ptr(), st.cuda_stream)
+    with pytest.raises(msv.MSVError):
+        e.check(st.cuda_stream)
+    e.check(st.cuda_stream)
+    assert np.array_equal(bits(d_sc.cpu().numpy()), bits(want))
+
+
 @pytest.mark.parametrize("length,n", [(400, 10_000), (2000, 2_500)])
 def test_viterbi_pvalues_calibrated_at_the_bench_lengths(length, n):
     """the Viterbi stage's P-values against STATS LOCAL VITERBI on iid background
@@ -483,18 +511,21 @@ def test_no_variant_keeps_its_rows_in_scratch():
     bitwise and is ~40x slower (round 5: a second instantiation of the single-wave row loop did that to
     S = 14..24 until the row lambdas were forced inline).  Pre-existing spills of the non-pick variants that
     run past the register file (S >= 32 at two waves per SIMD) stay below 1.2 KB and are listed here."""
-    # (round 5 build: bytes of private memory per lane, i.e. spilled VGPRs x 4 -- x 1.5 headroom; round 6 pruned
-    # the non-pick variants, so only the picks beyond the register file and the S = 22 W = 1 pick remain)
+    # (bytes of private memory per lane, i.e. spilled VGPRs x 4, as built -- x 1.5 headroom.  Round 6 pruned the
+    # non-pick variants, so only the picks beyond the register file and the S = 22 W = 1 pick remain; its W = 2
+    # exchange record (8 values per poll) took vit_w2_s13_ga4 from 40 to 84 bytes)
     allowed = {name: int(b * 1.5) for name, b in {
         "vit_s32_t0gi": 108, "vit_s64_t0g": 880, "vit_s64_t0gi": 1132,
-        "vit_w2_s12_ga4": 20, "vit_w2_s13_ga4": 40, "vit_w1_s22_ea": 36}.items()}
+        "vit_w2_s12_ga4": 20, "vit_w2_s13_ga4": 84, "vit_w1_s22_ea": 36}.items()}
     prof = "100.hmm"
-    bad = {}
+    bad, seen = {}, {}
     for name in msv.Viterbi_HMM.variants():
         e = msv.Viterbi_HMM(hmm(prof), insert_mode=1 if name.endswith("i") else 0)
         e.set_variant(name)
         info = e.describe()
         assert info["variant"] == name
+        seen[name] = info["scratch_bytes"]
         if info["scratch_bytes"] > allowed.get(name, 0):
             bad[name] = info["scratch_bytes"]
+    print({k: v for k, v in seen.items() if v})
     assert not bad, bad
