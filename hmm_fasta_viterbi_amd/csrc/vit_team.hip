@@ -76,7 +76,7 @@ struct TeamX {
 // lane 0's copy of a boundary is used (the DPP shift's `old` for wave 1's lane 0) and lane 0's stamp is the one
 // compared.  tests/test_team_exchange_isa.py checks in the gfx950 ISA that each record is one ds_write_b128 /
 // ds_write_b64 and each poll one ds_read_b128 / ds_read_b64 comparing that load's last dword.  (Stamping every
-// 8-byte half instead, which needs only 64-bit atomicity, was built in four forms and measured 3-8% slower on
+// 8-byte half instead, which needs only 64-bit atomicity, was built in seven forms and measured 3-9% slower on
 // cfg5's survivors: profiles/r06_ab/README.md.)
 typedef float v2f __attribute__((ext_vector_type(2)));
 typedef float v4f __attribute__((ext_vector_type(4)));

@@ -12,7 +12,7 @@ gfx950 (the library's own flags) and checks the ISA of every W = 2 team kernel:
 What the hardware must then provide is single-copy atomicity of one lane's aligned 16-byte (boundary) and 8-byte
 (E, next) LDS access; only lane 0's copy of the boundary is used (it enters lane 0 of wave 1 as the DPP shift's
 `old` operand) and its stamp is the one compared.  Per-half stamps that would need only 8-byte atomicity were
-built and measured: 3-8% slower on cfg5's survivors in every form (profiles/r06_ab/README.md), so the 16-byte
+built and measured: 3-9% slower on cfg5's survivors in every form (seven forms) (profiles/r06_ab/README.md), so the 16-byte
 record stays, guarded by this check."""
 import os
 import re
