@@ -117,3 +117,33 @@ def test_viterbi_entry_points_validate_arguments():
     assert L.msv_filter_select_device(0, None, None, None, 0, -9.0, 0.7, 0.02, None, None, cnt.ctypes.data,
                                       None) == 1
     assert L.msv_vit_profile_bind_stream(None, None) == 1
+
+
+def test_info_struct_layouts_match_the_header(tmp_path):
+    """The ctypes mirrors of msv_kernel_info / msv_vit_info (hmm_fasta_viterbi_amd/_native.py) have the C header's
+    field offsets and sizes (gcc on include/msv.h), and both structs keep their round-4 prefix: fields are only
+    appended (a field inserted mid-struct moved `variant` for C callers built against the old header)."""
+    import ctypes as C
+    structs = {"msv_kernel_info": _native.KernelInfo, "msv_vit_info": _native.VitInfo}
+    src = ['#include <stddef.h>', '#include <stdio.h>', '#include "msv.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        src.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            src.append(f'  printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    src.append("  return 0; }")
+    (tmp_path / "layout.c").write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", f"-I{os.path.join(ROOT, 'include')}", str(tmp_path / "layout.c"), "-o", str(exe)],
+                   check=True, capture_output=True)
+    got = {}
+    for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        s, f, v = line.split()
+        got[(s, f)] = int(v)
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == C.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
+    # the round-4 prefix of msv_vit_info: `variant` right after `device`, at byte 40
+    assert got[("msv_vit_info", "variant")] == 40
+    assert got[("msv_vit_info", "scratch_bytes")] > got[("msv_vit_info", "variant")]
+    assert got[("msv_vit_info", "waves_per_sequence")] > got[("msv_vit_info", "scratch_bytes")]
