@@ -273,6 +273,47 @@ def test_filter_select_device_order():
         assert cnt == len(w) and np.array_equal(d_sel[:cnt].cpu().numpy().view(np.uint32).astype(np.int64), w)
 
 
+def test_filter_select_device_many_blocks():
+    """the survivor compaction's block prefixes come from one scan workgroup (1,024 threads, each a
+    run of the counts) -- exercised past 1,024 blocks of 256 with runs of 10 and a ragged last block
+    (n = 2,600,003): the same survivors, in index order and in a given order, as the host formula."""
+    import torch
+    from hmm_fasta_viterbi_amd import _native
+    m = msv.MSV_HMM(hmm("400.hmm"))
+    n = 2_600_003
+    rng = np.random.Generator(np.random.PCG64(5))
+    lens = rng.integers(1, 600, n, dtype=np.int64)
+    offsets = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=offsets[1:])
+    sc = (m.msv_mu + rng.standard_normal(n) * 3.0).astype(np.float32)
+    F1 = 0.1
+    want = np.nonzero(m.pvalues(sc, offsets) <= F1)[0]
+    assert 1024 * 256 < n and 0 < len(want) < n
+    perm = rng.permutation(n).astype(np.uint32)
+    dev = torch.device("cuda:0")
+    d_sc = torch.from_numpy(sc).to(dev)
+    d_off = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    d_perm = torch.from_numpy(perm.view(np.int32)).to(dev)
+    d_sel = torch.empty(n, dtype=torch.int32, device=dev)
+    d_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    st = torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    L = _native.lib()
+    for order in (None, d_perm.data_ptr()):
+        _native.check(L.msv_filter_select_device(0, d_sc.data_ptr(), d_off.data_ptr(), order, n, m.msv_mu,
+                                                 m.msv_lambda, F1, None, d_sel.data_ptr(), d_cnt.data_ptr(),
+                                                 st.cuda_stream))
+        st.synchronize()
+        cnt = int(d_cnt.item())
+        got = d_sel[:cnt].cpu().numpy().view(np.uint32).astype(np.int64)
+        if order is None:
+            assert np.array_equal(got, want)
+        else:
+            keep = np.zeros(n, bool)
+            keep[want] = True
+            assert np.array_equal(got, perm.astype(np.int64)[keep[perm]])
+
+
 def test_filter_pipeline_matches_composition():
     """msv_vit_filter_batch (MSV -> P <= F1 -> Viterbi, on the device) = the oracle's MSV scores, the host
     P-value formula's pass mask, and the oracle's Viterbi scores on exactly those sequences."""
