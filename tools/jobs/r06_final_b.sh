@@ -28,3 +28,4 @@ for c in cfg3 cfg5; do
   python3 tools/pmc_summary.py $P ${c}_viterbi vit_team_kernel > $O/pmc_vit_$c.json
   rm -rf $P/pmc1 $P/pmc2 $P/pmc3 $P/trace
 done
+timeout -k 10 200 python -u -m pytest tests/test_gpu_viterbi.py -m gpu -x -q -k "many_blocks or clamped or filter_select" --timeout 150 --timeout-method thread > $O/pytest_new.log 2>&1
