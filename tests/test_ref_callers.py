@@ -103,3 +103,21 @@ def test_reference_benchmarks_run(tmp_path, name, n_lines):
             f.write(f"# {name}, cwd build/algorithms, wall {secs:.3f} s (process, incl. parse + profile uploads)\n")
             f.write(p.stdout)
     print(f"{name}: {len(best)} best-time lines, wall {secs:.2f} s")
+
+
+def test_integration_cmake_swap_builds_the_reference_tree(tmp_path):
+    """INTEGRATION.md §2 applied literally to a scratch copy of the reference tree (tests/ref_callers/cmake_swap.sh:
+    the reference's class sources deleted, its two library CMakeLists.txt replaced by INTERFACE targets on
+    include/drop_in + include + libmsv_hip.so): the reference's own CMake build (-Wall -Wextra -pedantic -Werror,
+    Debug) makes all six executables and its ctest parser tests pass.  The copy lives in pytest's tmp dir only."""
+    import shutil
+    if not os.path.isdir(os.path.join(REF, "algorithms")) or not shutil.which("cmake"):
+        pytest.skip("needs /root/reference and cmake (the build container)")
+    p = subprocess.run(["bash", os.path.join(ROOT, "tests", "ref_callers", "cmake_swap.sh"), str(tmp_path)],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
+    assert "100% tests passed" in p.stdout
+    built = (tmp_path / "make.log").read_text()
+    for target in ("test_MSV", "benchmark_MSV", "benchmark_MSV_1400", "test_hmm_parsing", "test_fasta_parsing",
+                   "HMM_FASTA_Viterbi"):
+        assert f"Built target {target}" in built, target
