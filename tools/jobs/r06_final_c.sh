@@ -1,0 +1,8 @@
+# Round 6, last GPU check at the final HEAD: the whole GPU suite (reference callers, speed gate, explicit-path
+# Viterbi pin, survivor compaction past 1,024 blocks included) and smoke.
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r06_final_c
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
